@@ -1,0 +1,149 @@
+"""ctypes front-end for the CPU parity checkers.  TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  The product package (sdfgen_amd) never does.
+
+* ``liboracle.so``  -- oracle/sdf_oracle.c, the C restatement of
+  cpu_lib/makelevelset3.cpp:192-304 (single-thread semantics).
+* ``_ref/libsdfref.so`` -- the reference's own cpu_lib/makelevelset3.cpp
+  compiled from /root/reference (development container only; absent on the
+  GPU box).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_ORACLE_SO = os.path.join(_HERE, "liboracle.so")
+_REF_SO = os.path.join(_HERE, "_ref", "libsdfref.so")
+
+_P = ctypes.c_void_p
+_oracle = None
+_ref = None
+
+
+def build(ref: bool = False) -> None:
+    """Compile the C restatement (and, if asked and available, the reference)."""
+    targets = ["all"] + (["ref"] if ref else [])
+    subprocess.run(["make", "-s", "-C", _HERE] + targets, check=True)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(_P)
+
+
+def lib():
+    global _oracle
+    if _oracle is None:
+        if not os.path.exists(_ORACLE_SO):
+            build()
+        L = ctypes.CDLL(_ORACLE_SO)
+        L.oracle_make_level_set3.argtypes = [_P, ctypes.c_uint64, _P, ctypes.c_uint64, _P, ctypes.c_float,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P]
+        L.oracle_make_level_set3.restype = ctypes.c_int
+        L.oracle_band.argtypes = [_P, ctypes.c_uint64, _P, ctypes.c_uint64, _P, ctypes.c_float,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P]
+        L.oracle_band.restype = ctypes.c_int
+        L.oracle_sweep.argtypes = [_P, _P, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   _P, _P, ctypes.c_int]
+        L.oracle_sweep.restype = None
+        L.oracle_sign.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P]
+        L.oracle_sign.restype = None
+        L.oracle_ptd_batch.argtypes = [ctypes.c_uint64, _P, _P]
+        L.oracle_ptd_batch.restype = None
+        _oracle = L
+    return _oracle
+
+
+def ref_available() -> bool:
+    return os.path.exists(_REF_SO)
+
+
+def ref_lib():
+    global _ref
+    if _ref is None:
+        if not os.path.exists(_REF_SO):
+            raise FileNotFoundError(f"{_REF_SO} not built (needs /root/reference; `make -C oracle ref`)")
+        L = ctypes.CDLL(_REF_SO)
+        L.ref_make_level_set3.argtypes = [_P, ctypes.c_uint64, _P, ctypes.c_uint64, _P, ctypes.c_float,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, _P]
+        L.ref_make_level_set3.restype = ctypes.c_int
+        L.ref_ptd_batch.argtypes = [ctypes.c_uint64, _P, _P]
+        L.ref_ptd_batch.restype = None
+        L.ref_pit2d_batch.argtypes = [ctypes.c_uint64, _P, _P]
+        L.ref_pit2d_batch.restype = None
+        _ref = L
+    return _ref
+
+
+def _prep(vertices, triangles, origin):
+    v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    t = np.ascontiguousarray(triangles, dtype=np.uint32).reshape(-1, 3)
+    o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+    return v, t, o
+
+
+def make_level_set3(vertices, triangles, origin, dx, ni, nj, nk, exact_band=1) -> np.ndarray:
+    """Oracle phi, returned as a (ni, nj, nk) view of the i-fastest Array3f buffer
+    (i.e. phi[i, j, k] == Array3f(i, j, k)); Fortran-ordered."""
+    v, t, o = _prep(vertices, triangles, origin)
+    out = np.empty(ni * nj * nk, dtype=np.float32)
+    rc = lib().oracle_make_level_set3(_ptr(t), t.shape[0], _ptr(v), v.shape[0], _ptr(o),
+                                      ctypes.c_float(dx), ni, nj, nk, exact_band, _ptr(out))
+    if rc != 0:
+        raise ValueError(f"oracle_make_level_set3 failed rc={rc}")
+    return out.reshape((ni, nj, nk), order="F")
+
+
+def band(vertices, triangles, origin, dx, ni, nj, nk, exact_band=1):
+    """Stage 1 only: (phi, closest_tri, intersection_count), each (ni,nj,nk) F-order."""
+    v, t, o = _prep(vertices, triangles, origin)
+    n = ni * nj * nk
+    phi = np.empty(n, np.float32)
+    ct = np.empty(n, np.int32)
+    cnt = np.empty(n, np.int32)
+    rc = lib().oracle_band(_ptr(t), t.shape[0], _ptr(v), v.shape[0], _ptr(o), ctypes.c_float(dx),
+                           ni, nj, nk, exact_band, _ptr(phi), _ptr(ct), _ptr(cnt))
+    if rc != 0:
+        raise ValueError(f"oracle_band failed rc={rc}")
+    f = lambda a: a.reshape((ni, nj, nk), order="F")
+    return f(phi), f(ct), f(cnt)
+
+
+def sweep(vertices, triangles, origin, dx, phi, ct, nsweeps=16):
+    """Stage 2 in place on F-ordered (ni,nj,nk) phi / ct arrays (returns copies)."""
+    v, t, o = _prep(vertices, triangles, origin)
+    ni, nj, nk = phi.shape
+    p = np.asfortranarray(phi, dtype=np.float32).copy(order="F")
+    c = np.asfortranarray(ct, dtype=np.int32).copy(order="F")
+    lib().oracle_sweep(_ptr(t), _ptr(v), _ptr(o), ctypes.c_float(dx), ni, nj, nk,
+                       p.ctypes.data_as(_P), c.ctypes.data_as(_P), nsweeps)
+    return p, c
+
+
+def ptd_batch(pts: np.ndarray) -> np.ndarray:
+    pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 12)
+    out = np.empty(pts.shape[0], np.float32)
+    lib().oracle_ptd_batch(pts.shape[0], _ptr(pts), _ptr(out))
+    return out
+
+
+def ref_make_level_set3(vertices, triangles, origin, dx, ni, nj, nk, exact_band=1, num_threads=1):
+    """The REFERENCE implementation (development container only)."""
+    v, t, o = _prep(vertices, triangles, origin)
+    out = np.empty(ni * nj * nk, dtype=np.float32)
+    ref_lib().ref_make_level_set3(_ptr(t), t.shape[0], _ptr(v), v.shape[0], _ptr(o), ctypes.c_float(dx),
+                                  ni, nj, nk, exact_band, num_threads, _ptr(out))
+    return out.reshape((ni, nj, nk), order="F")
+
+
+def ref_ptd_batch(pts: np.ndarray) -> np.ndarray:
+    pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 12)
+    out = np.empty(pts.shape[0], np.float32)
+    ref_lib().ref_ptd_batch(pts.shape[0], _ptr(pts), _ptr(out))
+    return out

@@ -1,0 +1,205 @@
+"""Host-side mesh and .sdf file I/O (the callers either side of the hot path).
+
+These restate the reference's loaders/writers with bulk numpy I/O instead of
+per-value stream calls:
+
+* ``load_mesh``  -- common/mesh_io.cpp:29-48 dispatch on extension;
+  binary STL common/mesh_io_stl.cpp:98-173 (no vertex de-duplication:
+  vertices 3t, 3t+1, 3t+2 per facet), ASCII STL :179-303, format detection
+  :42-92, OBJ common/mesh_io_obj.cpp:21-157 (fan triangulation :115-121).
+  Bounds follow update_minmax (common/mesh_io.h:101-108).
+* ``write_sdf`` / ``read_sdf`` -- common/sdf_io.cpp:10-147: a 36-byte header
+  (3 x int32 dims, 3 x f32 min, 3 x f32 max = min + n*dx) followed by float32
+  data written k-fastest (for i, for j, for k), i.e. exactly a C-ordered
+  (ni, nj, nk) numpy array -- one bulk write instead of one 4-byte write per
+  value.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+
+import numpy as np
+
+_STL_HEADER = 80
+_STL_TRI = 50
+_FLT_MAX = np.finfo(np.float32).max
+
+_libc = ctypes.CDLL(None)
+_libc.strtof.restype = ctypes.c_float
+_libc.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
+
+
+def _parse_f32(tok: str) -> np.float32:
+    # C++ `istream >> float` is strtof-correct rounding; float(tok) then a cast
+    # to float32 would double-round.
+    end = ctypes.c_char_p()
+    b = tok.encode()
+    v = _libc.strtof(b, ctypes.byref(end))
+    return np.float32(v)
+
+
+def _bounds(v: np.ndarray):
+    if v.shape[0] == 0:
+        mn = np.full(3, _FLT_MAX, np.float32)
+        mx = np.full(3, -_FLT_MAX, np.float32)
+    else:
+        mn = np.fmin.reduce(v, axis=0).astype(np.float32)
+        mx = np.fmax.reduce(v, axis=0).astype(np.float32)
+    return (tuple(float(a) for a in mn), tuple(float(a) for a in mx))
+
+
+def _stl_is_binary(path: str) -> bool:
+    with open(path, "rb") as f:
+        head = f.read(_STL_HEADER)
+        if len(head) < 5:
+            raise RuntimeError(f"Failed to load mesh: {path}")
+        if not head.lower().startswith(b"solid"):
+            return True
+        cnt = f.read(4)
+        if len(cnt) < 4:
+            return False
+        (n,) = struct.unpack("<I", cnt)
+    return os.path.getsize(path) == _STL_HEADER + 4 + n * _STL_TRI
+
+
+def _load_binary_stl(path: str):
+    with open(path, "rb") as f:
+        f.seek(_STL_HEADER)
+        cnt = f.read(4)
+        if len(cnt) < 4:
+            raise RuntimeError(f"Failed to load mesh: {path}")
+        (n,) = struct.unpack("<I", cnt)
+        raw = np.fromfile(f, dtype=np.uint8, count=n * _STL_TRI)
+    if raw.size < n * _STL_TRI:
+        raise RuntimeError(f"Failed to load mesh: {path} (truncated binary STL)")
+    rec = raw.reshape(n, _STL_TRI)
+    verts = rec[:, 12:48].copy().view("<f4").reshape(n * 3, 3).astype(np.float32)
+    tris = np.arange(n * 3, dtype=np.uint32).reshape(n, 3)
+    return verts, tris
+
+
+def _load_ascii_stl(path: str):
+    verts = []
+    ntri = 0
+    in_facet = in_loop = False
+    nv = 0
+    with open(path, "r", errors="replace") as f:
+        for line in f:
+            s = line.strip()
+            low = s.lower()
+            if low.startswith("facet"):
+                in_facet, nv = True, 0
+            elif low.startswith("endfacet"):
+                if nv != 3:
+                    raise RuntimeError(f"Failed to load mesh: {path} (facet with {nv} vertices)")
+                in_facet = False
+                ntri += 1
+            elif low.startswith("outer loop"):
+                in_loop = True
+            elif low.startswith("endloop"):
+                in_loop = False
+            elif low.startswith("vertex"):
+                if not (in_facet and in_loop):
+                    raise RuntimeError(f"Failed to load mesh: {path} (vertex outside facet)")
+                tok = s.split()
+                if len(tok) < 4:
+                    raise RuntimeError(f"Failed to load mesh: {path} (bad vertex line)")
+                verts.append([_parse_f32(t) for t in tok[1:4]])
+                nv += 1
+    if not verts or ntri == 0:
+        raise RuntimeError(f"Failed to load mesh: {path} (no facets)")
+    v = np.asarray(verts, dtype=np.float32).reshape(-1, 3)
+    t = np.arange(ntri * 3, dtype=np.uint32).reshape(ntri, 3)
+    return v, t
+
+
+def _load_obj(path: str):
+    verts = []
+    faces = []
+    with open(path, "r", errors="replace") as f:
+        for line in f:
+            line = line.rstrip("\n").rstrip("\r")
+            if not line:
+                continue
+            if line[0] == "v" and len(line) > 1 and line[1] in " \t":
+                tok = line.split()
+                if len(tok) < 4:
+                    continue
+                verts.append([_parse_f32(t) for t in tok[1:4]])
+            elif line[0] == "f" and len(line) > 1 and line[1] in " \t":
+                idx = [int(t.split("/")[0]) for t in line.split()[1:]]
+                if len(idx) < 3:
+                    continue
+                for q in range(1, len(idx) - 1):  # fan, mesh_io_obj.cpp:115-121
+                    faces.append([(idx[0] - 1) & 0xFFFFFFFF, (idx[q] - 1) & 0xFFFFFFFF,
+                                  (idx[q + 1] - 1) & 0xFFFFFFFF])
+    if not verts or not faces:
+        raise RuntimeError(f"Failed to load mesh: {path} (no vertices or faces)")
+    return np.asarray(verts, np.float32).reshape(-1, 3), np.asarray(faces, np.uint32).reshape(-1, 3)
+
+
+def load_mesh(filename: str):
+    """Load an OBJ or STL mesh -> (vertices (N,3) f32, triangles (M,3) u32, bounds).
+
+    Mirrors python/sdfgen_py.cpp:101-157 (``sdfgen.load_mesh``)."""
+    path = os.fspath(filename)
+    ext = os.path.splitext(path)[1].lower()
+    if not os.path.isfile(path):
+        raise RuntimeError(f"Failed to load mesh: {path}")
+    try:
+        if ext == ".stl":
+            v, t = _load_binary_stl(path) if _stl_is_binary(path) else _load_ascii_stl(path)
+        elif ext == ".obj":
+            v, t = _load_obj(path)
+        else:
+            raise RuntimeError(f"Failed to load mesh: {path} (unsupported format {ext})")
+    except (ValueError, UnicodeDecodeError) as e:
+        raise RuntimeError(f"Failed to load mesh: {path} ({e})") from e
+    return v, t, _bounds(v)
+
+
+def write_sdf(filename: str, sdf: np.ndarray, origin, dx: float) -> int:
+    """Write ``sdf`` (C-ordered (ni,nj,nk) float32) as a .sdf file; returns the
+    inside count (``val < 0``, common/sdf_io.cpp:53)."""
+    a = np.ascontiguousarray(sdf, dtype=np.float32)
+    if a.ndim != 3:
+        raise ValueError("SDF array must be 3-dimensional")
+    ni, nj, nk = a.shape
+    if ni == 0 or nj == 0 or nk == 0:
+        raise ValueError("SDF array dimensions cannot be zero")
+    o = np.asarray(origin, dtype=np.float32).reshape(3)
+    dxf = np.float32(dx)
+    mx = np.array([o[0] + np.float32(ni) * dxf, o[1] + np.float32(nj) * dxf, o[2] + np.float32(nk) * dxf],
+                  dtype=np.float32)
+    try:
+        with open(filename, "wb") as f:
+            f.write(struct.pack("<3i", ni, nj, nk))
+            f.write(o.astype("<f4").tobytes())
+            f.write(mx.astype("<f4").tobytes())
+            a.astype("<f4", copy=False).tofile(f)
+    except OSError as e:
+        raise RuntimeError(f"Failed to write SDF file: {filename}") from e
+    return int(np.count_nonzero(a < 0.0))
+
+
+def read_sdf(filename: str):
+    """Read a .sdf file -> (sdf (ni,nj,nk) float32 C-order, min_box, max_box)."""
+    try:
+        with open(filename, "rb") as f:
+            head = f.read(36)
+            if len(head) < 36:
+                raise RuntimeError(f"Failed to read SDF file: {filename}")
+            ni, nj, nk = struct.unpack("<3i", head[:12])
+            if ni <= 0 or nj <= 0 or nk <= 0:
+                raise RuntimeError(f"Failed to read SDF file: {filename} (bad dims)")
+            mn = struct.unpack("<3f", head[12:24])
+            mx = struct.unpack("<3f", head[24:36])
+            n = ni * nj * nk
+            data = np.fromfile(f, dtype="<f4", count=n)
+    except OSError as e:
+        raise RuntimeError(f"Failed to read SDF file: {filename}") from e
+    if data.size != n:
+        raise RuntimeError(f"Failed to read SDF file: {filename} (truncated)")
+    return data.astype(np.float32).reshape(ni, nj, nk), mn, mx
