@@ -1,0 +1,167 @@
+"""Benchmark: make_level_set3 on MI355X (BASELINE.json metric: Mvoxels/s at 256^3, 1M-tri mesh).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload NAME]
+
+One step = one complete make_level_set3 (prep, band + ray parity, 16 sweeps,
+sign) on the deterministic 1M-triangle bumpy sphere with inputs already
+resident in HBM and phi written to HBM (sdfgen_hip_make_level_set3_device).
+For N > 1 (launched by torch.distributed.run), every rank runs the same
+single-GPU job on its own GPU ("replicas", weak scaling); see DESIGN.md.
+
+Rank 0 prints one JSON line with the driver's contract fields plus
+`roofline` (dominant kernel = the sweep, HIP-event timed inside the library
+on the launch stream) and `cpu_baseline` (the oracle, 1 thread, on a bounded
+sample; N=1 only).
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "Mvoxels/sec at 256³ (1M-tri mesh); achieved HBM GB/s vs peak"
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SWEEP_BYTES_PER_CELL = 16   # read phi+ct (8 B) + write phi+ct (8 B) per cell per sweep
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(workload: str):
+    """Oracle (oracle/sdf_oracle.c, 1 thread) on a bounded sample: the same 1M-triangle
+    mesh on a 128^3 grid (same mode-2b recipe) -- about 15 s of CPU work."""
+    from oracle import oracle as O
+    from sdfgen_amd import meshgen
+
+    w = meshgen.WORKLOADS[workload]
+    v, t = meshgen.bumpy_sphere(w["nu"], w["nv"])
+    n = 128
+    o, dx = meshgen.grid_mode2b(v, n, n, n, w["padding"])
+    t0 = time.perf_counter()
+    O.make_level_set3(v, t, o, dx, n, n, n, 1)
+    el = time.perf_counter() - t0
+    return {"value": round(n ** 3 / el / 1e6, 4), "unit": "Mvoxels/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/sdf_oracle.c single-thread, same {t.shape[0]}-triangle mesh on a {n}^3 grid "
+                      f"({n ** 3} voxels), {el:.2f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c3_sphere1m_256")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    from sdfgen_amd import _lib, meshgen
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device(f"cuda:{local_rank}")
+
+    v, t, o, dx, dims = meshgen.workload(args.workload)
+    ni, nj, nk = dims
+    ncell = ni * nj * nk
+    dv = torch.from_numpy(v).to(dev)
+    dt = torch.from_numpy(t.view(np.int32)).to(dev)
+    out = torch.empty(ncell, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        _lib.make_level_set3_device(local_rank, dt.data_ptr(), t.shape[0], dv.data_ptr(), v.shape[0], o, dx,
+                                    ni, nj, nk, 1, _lib.LAYOUT_ARRAY3, out.data_ptr(), stream.cuda_stream)
+        return _lib.last_profile()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    profs = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        x = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        el = float(x.item())
+
+    ms_step = el / args.steps * 1e3
+    value = world * ncell * args.steps / el / 1e6
+    # dominant kernel: the sweep.  Per-launch duration from the library's HIP events on the launch stream.
+    sweep_ms = sum(p["sweep_ms"] for p in profs) / len(profs)
+    launches = profs[-1]["sweep_launches"]
+    A, B, C = ni - 1, nj - 1, nk - 1
+    bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * C * 16 / max(launches, 1)
+    launch_ms = sweep_ms / max(launches, 1)
+    achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    phases = {k: round(sum(p[k] for p in profs) / len(profs), 4)
+              for k in ("prep_ms", "band_ms", "sweep_ms", "sign_ms", "total_ms")}
+
+    parity = None
+    if not args.no_verify and rank == 0:
+        hp = os.path.join(ROOT, "tests", "golden", "hashes.json")
+        if os.path.exists(hp):
+            rec = json.load(open(hp)).get(args.workload)
+            if rec:
+                got = out.cpu().numpy()
+                ok = hashlib.sha256(got.astype("<f4").tobytes()).hexdigest() == rec["sha256_phi"]
+                parity = "bit-exact vs reference (sha256 of phi)" if ok else "MISMATCH vs reference sha256"
+
+    if rank == 0:
+        res = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mvoxels/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic 1M-triangle bumpy UV-sphere, sdfgen_amd/meshgen.py)",
+            "config": {"workload": args.workload, "grid": list(dims), "triangles": int(t.shape[0]),
+                       "exact_band": 1, "parallelism": "replicas" if world > 1 else "single-gpu",
+                       "inputs": "HBM-resident"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "sweep", "launches_per_step": launches,
+                         "avg_launch_ms": round(launch_ms, 5),
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+            "phases_ms": phases,
+            "sweep_impl": profs[-1]["sweep_impl"],
+            "parity": parity,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(args.workload)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

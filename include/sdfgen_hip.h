@@ -1,0 +1,119 @@
+/*
+ * sdfgen_hip.h -- C-ABI of the MI355X (gfx950) signed-distance-field backend.
+ *
+ * This is the drop-in boundary for the reference's hot path
+ *   sdfgen::make_level_set3(tri, x, origin, dx, nx, ny, nz, phi, exact_band,
+ *                           HardwareBackend, num_threads)
+ *     declared   /root/reference/common/sdfgen_unified.h:47-57
+ *     dispatched /root/reference/common/sdfgen_unified.cpp:30-71
+ *     GPU case   /root/reference/gpu_lib/makelevelset3_gpu.h:40-42 (gpu::make_level_set3)
+ *   sdfgen::is_gpu_available()   common/sdfgen_unified.h:68, .cpp:19-28
+ * Plain pointers and sizes only; no C++ or torch types cross it.  A reference
+ * maintainer binds it from gpu_lib (C++), python/sdfgen_py.cpp (nanobind) or
+ * ctypes -- see INTEGRATION.md.
+ *
+ * Semantics: results are bit-identical to the reference's single-threaded CPU
+ * implementation cpu_lib/makelevelset3.cpp:192-304 (distances, closest-triangle
+ * tie-breaks and the -0.0 produced by the sign flip), NOT to the reference CUDA
+ * backend, whose far field is a different (Eikonal) algorithm.
+ *
+ * Contract for every entry point:
+ *   - returns SDFGEN_HIP_OK (0) on success, a negative SDFGEN_HIP_E* code
+ *     otherwise, with a NUL-terminated message in errbuf (if errbuf != NULL);
+ *   - never calls exit()/abort(), never retains caller pointers after return;
+ *   - synchronous on return (host entry points), reentrant (serialised per
+ *     device internally).
+ */
+#ifndef SDFGEN_HIP_H
+#define SDFGEN_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDFGEN_HIP_ABI_VERSION 1
+
+enum {
+    SDFGEN_HIP_OK = 0,
+    SDFGEN_HIP_EINVAL = -1,      /* bad argument (dims <= 0, dx <= 0 / non-finite, layout, ...) */
+    SDFGEN_HIP_EINDEX = -2,      /* a triangle references a vertex index >= nvert */
+    SDFGEN_HIP_ENODEV = -3,      /* no usable HIP device */
+    SDFGEN_HIP_ERUNTIME = -4,    /* HIP runtime / kernel error */
+    SDFGEN_HIP_ENOMEM = -5       /* device allocation failed */
+};
+
+/* Output layouts for phi_out. */
+enum {
+    SDFGEN_LAYOUT_ARRAY3 = 0,    /* i-fastest: phi[i + ni*(j + nj*k)] (Array3f, common/array3.h:114) */
+    SDFGEN_LAYOUT_KFAST = 1      /* k-fastest: phi[(i*nj + j)*nk + k] (numpy (ni,nj,nk) C-order and
+                                    the .sdf body, python/sdfgen_py.cpp:80-86, common/sdf_io.cpp:49-57) */
+};
+
+int sdfgen_hip_abi_version(void);
+
+/* Number of visible HIP devices (0 when none; never an error).
+ * Replaces sdfgen::is_gpu_available() (common/sdfgen_unified.cpp:19-28). */
+int sdfgen_hip_device_count(void);
+
+/*
+ * Host-memory entry point; replaces gpu::make_level_set3 (gpu_lib/makelevelset3_gpu.cu:595-777).
+ *   tri      : ntri x 3 uint32 vertex indices (std::vector<Vec3ui>::data(), common/vec.h:28)
+ *   xyz      : nvert x 3 float32 positions   (std::vector<Vec3f>::data())
+ *   origin   : grid origin (3 floats); dx: cell size; ni,nj,nk: grid dims (> 0)
+ *   exact_band: band half-width in cells (cpu_lib/makelevelset3.cpp:210-212)
+ *   ngpu     : devices to use (0 = all visible; the grid is split into Z-slabs)
+ *   out_layout: SDFGEN_LAYOUT_*
+ *   phi_out  : caller-allocated ni*nj*nk floats
+ */
+int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert,
+                               const float origin[3], float dx, int ni, int nj, int nk,
+                               int exact_band, int ngpu, int out_layout, float *phi_out,
+                               char *errbuf, size_t errlen);
+
+/*
+ * Device-resident entry point (inputs already in HBM of `device`): the same
+ * computation on caller-owned device buffers, enqueued on `hip_stream`
+ * (a hipStream_t; NULL = the library's own stream) and synchronised before
+ * return.  d_phi_out: ni*nj*nk floats on `device`.
+ */
+int sdfgen_hip_make_level_set3_device(int device, const uint32_t *d_tri, uint64_t ntri,
+                                      const float *d_xyz, uint64_t nvert, const float origin[3],
+                                      float dx, int ni, int nj, int nk, int exact_band,
+                                      int out_layout, float *d_phi_out, void *hip_stream,
+                                      char *errbuf, size_t errlen);
+
+/* Per-phase device timings of the last call on the calling process (HIP events
+ * recorded on the launch stream around each phase / sweep launch). */
+typedef struct sdfgen_hip_profile {
+    double total_ms;          /* first kernel start .. last kernel end */
+    double prep_ms;           /* triangle gather + workspace init */
+    double band_ms;           /* narrow band + ray-parity counts */
+    double sweep_ms;          /* all 16 sweeps */
+    double sign_ms;           /* sign pass + output layout */
+    double sweep_launch_ms[16];  /* per (pass, direction) sweep */
+    int sweep_launches;       /* kernel launches issued for the sweeps */
+    int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined column wavefront */
+    uint64_t band_evals;      /* point-triangle evaluations in the band phase */
+    uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless counting enabled) */
+} sdfgen_hip_profile;
+
+int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
+
+/* Free cached device workspaces (they are grow-only between calls). */
+int sdfgen_hip_release(void);
+
+/* Diagnostics (used by the parity tests): evaluate the device geometry kernels
+ * on host arrays.  pts: n x 12 floats (x0,x1,x2,x3) -> out: n floats.
+ * pit: n x 8 doubles (x0,y0,x1,y1,x2,y2,x3,y3) -> out4: n x (flag,a,b,c). */
+int sdfgen_hip_debug_ptd(int device, uint64_t n, const float *pts, float *out,
+                         char *errbuf, size_t errlen);
+int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *out4,
+                           char *errbuf, size_t errlen);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDFGEN_HIP_H */

@@ -55,6 +55,8 @@ def lib():
         L.oracle_sign.restype = None
         L.oracle_ptd_batch.argtypes = [ctypes.c_uint64, _P, _P]
         L.oracle_ptd_batch.restype = None
+        L.oracle_pit2d_batch.argtypes = [ctypes.c_uint64, _P, _P]
+        L.oracle_pit2d_batch.restype = None
         _oracle = L
     return _oracle
 
@@ -130,6 +132,20 @@ def ptd_batch(pts: np.ndarray) -> np.ndarray:
     pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 12)
     out = np.empty(pts.shape[0], np.float32)
     lib().oracle_ptd_batch(pts.shape[0], _ptr(pts), _ptr(out))
+    return out
+
+
+def pit2d_batch(pit: np.ndarray) -> np.ndarray:
+    pit = np.ascontiguousarray(pit, dtype=np.float64).reshape(-1, 8)
+    out = np.empty((pit.shape[0], 4), np.float64)
+    lib().oracle_pit2d_batch(pit.shape[0], _ptr(pit), _ptr(out))
+    return out
+
+
+def ref_pit2d_batch(pit: np.ndarray) -> np.ndarray:
+    pit = np.ascontiguousarray(pit, dtype=np.float64).reshape(-1, 8)
+    out = np.empty((pit.shape[0], 4), np.float64)
+    ref_lib().ref_pit2d_batch(pit.shape[0], _ptr(pit), _ptr(out))
     return out
 
 

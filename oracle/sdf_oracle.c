@@ -294,3 +294,17 @@ void oracle_ptd_batch(uint64_t n, const float *pts, float *out)
         out[q] = oracle_ptd(p, p + 3, p + 6, p + 9);
     }
 }
+
+/* Batched point_in_triangle_2d: in = n x 8 doubles, out = n x (flag, a, b, c). */
+void oracle_pit2d_batch(uint64_t n, const double *in, double *out)
+{
+    for (uint64_t q = 0; q < n; ++q) {
+        const double *p = in + 8 * q;
+        double a = 0, b = 0, c = 0;
+        int r = oracle_pit2d(p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], &a, &b, &c);
+        out[4 * q] = r ? 1.0 : 0.0;
+        out[4 * q + 1] = a;
+        out[4 * q + 2] = b;
+        out[4 * q + 3] = c;
+    }
+}

@@ -1,0 +1,195 @@
+"""ctypes binding of the C-ABI in include/sdfgen_hip.h (libsdfgen_hip.so, built in-tree).
+
+The product path: every generate call goes through this library.  There is no
+CPU fallback here -- if the shared library is missing, importing this module
+raises ImportError, and a GPU request without a usable device raises
+RuntimeError (the reference's "GPU requested but unavailable" contract,
+common/sdfgen_unified.cpp:60-63; python/tests/test_sdfgen.py:1030-1049).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsdfgen_hip.so")
+
+OK, EINVAL, EINDEX, ENODEV, ERUNTIME, ENOMEM = 0, -1, -2, -3, -4, -5
+LAYOUT_ARRAY3, LAYOUT_KFAST = 0, 1
+
+_P = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+
+# Every symbol include/sdfgen_hip.h declares (checked by tests/test_abi.py).
+EXPORTED = (
+    "sdfgen_hip_abi_version",
+    "sdfgen_hip_device_count",
+    "sdfgen_hip_make_level_set3",
+    "sdfgen_hip_make_level_set3_device",
+    "sdfgen_hip_last_profile",
+    "sdfgen_hip_release",
+    "sdfgen_hip_debug_ptd",
+    "sdfgen_hip_debug_pit2d",
+    "sdfgen_cpu_make_level_set3",
+)
+
+
+class Profile(ctypes.Structure):
+    _fields_ = [
+        ("total_ms", ctypes.c_double),
+        ("prep_ms", ctypes.c_double),
+        ("band_ms", ctypes.c_double),
+        ("sweep_ms", ctypes.c_double),
+        ("sign_ms", ctypes.c_double),
+        ("sweep_launch_ms", ctypes.c_double * 16),
+        ("sweep_launches", ctypes.c_int),
+        ("sweep_impl", ctypes.c_int),
+        ("band_evals", ctypes.c_uint64),
+        ("sweep_evals", ctypes.c_uint64),
+    ]
+
+    def as_dict(self):
+        d = {f: getattr(self, f) for f, _ in self._fields_}
+        d["sweep_launch_ms"] = list(self.sweep_launch_ms)
+        return d
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build the HIP backend first "
+            "(python -c 'import __graft_entry__ as g; g.build()' or make -C sdfgen_amd)")
+    L = ctypes.CDLL(LIB_PATH)
+    L.sdfgen_hip_abi_version.restype = ctypes.c_int
+    L.sdfgen_hip_device_count.restype = ctypes.c_int
+    L.sdfgen_hip_make_level_set3.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
+                                             ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_hip_make_level_set3.restype = ctypes.c_int
+    L.sdfgen_hip_make_level_set3_device.argtypes = [ctypes.c_int, _P, _u64, _P, _u64, _P, ctypes.c_float,
+                                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_hip_make_level_set3_device.restype = ctypes.c_int
+    L.sdfgen_hip_last_profile.argtypes = [ctypes.POINTER(Profile)]
+    L.sdfgen_hip_last_profile.restype = ctypes.c_int
+    L.sdfgen_hip_release.restype = ctypes.c_int
+    L.sdfgen_cpu_make_level_set3.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
+                                             ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_cpu_make_level_set3.restype = ctypes.c_int
+    L.sdfgen_hip_debug_ptd.argtypes = [ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_hip_debug_ptd.restype = ctypes.c_int
+    L.sdfgen_hip_debug_pit2d.argtypes = [ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_hip_debug_pit2d.restype = ctypes.c_int
+    return L
+
+
+lib = _load()
+
+
+class HipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
+
+def _raise(code: int, buf) -> None:
+    msg = buf.value.decode(errors="replace") if buf is not None else ""
+    if code == EINVAL:
+        raise ValueError(msg or "invalid argument")
+    if code == EINDEX:
+        raise IndexError(msg or "triangle vertex index out of range")
+    if code == ENODEV:
+        raise RuntimeError(msg or "GPU backend requested but no HIP GPU is available")
+    raise HipError(code, msg or f"GPU (HIP) backend error {code}")
+
+
+def device_count() -> int:
+    return int(lib.sdfgen_hip_device_count())
+
+
+def make_level_set3(vertices: np.ndarray, triangles: np.ndarray, origin, dx: float, ni: int, nj: int, nk: int,
+                    exact_band: int = 1, layout: int = LAYOUT_KFAST, ngpu: int = 0) -> np.ndarray:
+    """Host-memory entry (sdfgen_hip_make_level_set3).  Returns phi as a (ni,nj,nk)
+    array: C-ordered for LAYOUT_KFAST, a Fortran-ordered view of the i-fastest
+    Array3f buffer for LAYOUT_ARRAY3 -- either way phi[i, j, k]."""
+    v = np.ascontiguousarray(vertices, dtype=np.float32)
+    t = np.ascontiguousarray(triangles, dtype=np.uint32)
+    o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+    out = np.empty(int(ni) * int(nj) * int(nk), dtype=np.float32)
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_hip_make_level_set3(t.ctypes.data_as(_P), t.shape[0] if t.ndim == 2 else t.size // 3,
+                                        v.ctypes.data_as(_P), v.shape[0] if v.ndim == 2 else v.size // 3,
+                                        o.ctypes.data_as(_P), ctypes.c_float(dx), int(ni), int(nj), int(nk),
+                                        int(exact_band), int(ngpu), int(layout), out.ctypes.data_as(_P), err,
+                                        ctypes.sizeof(err))
+    if rc != OK:
+        _raise(rc, err)
+    if layout == LAYOUT_KFAST:
+        return out.reshape((ni, nj, nk))
+    return out.reshape((ni, nj, nk), order="F")
+
+
+def cpu_make_level_set3(vertices: np.ndarray, triangles: np.ndarray, origin, dx: float, ni: int, nj: int, nk: int,
+                        exact_band: int = 1, num_threads: int = 0, layout: int = LAYOUT_KFAST) -> np.ndarray:
+    """The library's native CPU backend (include/sdfgen_cpu.h); same return convention."""
+    v = np.ascontiguousarray(vertices, dtype=np.float32)
+    t = np.ascontiguousarray(triangles, dtype=np.uint32)
+    o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+    out = np.empty(int(ni) * int(nj) * int(nk), dtype=np.float32)
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_cpu_make_level_set3(t.ctypes.data_as(_P), t.size // 3, v.ctypes.data_as(_P), v.size // 3,
+                                        o.ctypes.data_as(_P), ctypes.c_float(dx), int(ni), int(nj), int(nk),
+                                        int(exact_band), int(num_threads), int(layout), out.ctypes.data_as(_P),
+                                        err, ctypes.sizeof(err))
+    if rc != OK:
+        _raise(rc, err)
+    if layout == LAYOUT_KFAST:
+        return out.reshape((ni, nj, nk))
+    return out.reshape((ni, nj, nk), order="F")
+
+
+def make_level_set3_device(device: int, d_tri: int, ntri: int, d_xyz: int, nvert: int, origin, dx: float,
+                           ni: int, nj: int, nk: int, exact_band: int, layout: int, d_out: int,
+                           stream: int = 0) -> None:
+    """Device-resident entry: raw device pointers (ints), optional hipStream_t."""
+    o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_hip_make_level_set3_device(int(device), _P(d_tri), int(ntri), _P(d_xyz), int(nvert),
+                                               o.ctypes.data_as(_P), ctypes.c_float(dx), int(ni), int(nj),
+                                               int(nk), int(exact_band), int(layout), _P(d_out),
+                                               _P(stream) if stream else None, err, ctypes.sizeof(err))
+    if rc != OK:
+        _raise(rc, err)
+
+
+def last_profile() -> dict:
+    p = Profile()
+    lib.sdfgen_hip_last_profile(ctypes.byref(p))
+    return p.as_dict()
+
+
+def release() -> None:
+    lib.sdfgen_hip_release()
+
+
+def debug_ptd(pts: np.ndarray, device: int = 0) -> np.ndarray:
+    pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 12)
+    out = np.empty(pts.shape[0], np.float32)
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_hip_debug_ptd(device, pts.shape[0], pts.ctypes.data_as(_P), out.ctypes.data_as(_P), err, 512)
+    if rc != OK:
+        _raise(rc, err)
+    return out
+
+
+def debug_pit2d(pit: np.ndarray, device: int = 0) -> np.ndarray:
+    pit = np.ascontiguousarray(pit, dtype=np.float64).reshape(-1, 8)
+    out = np.empty((pit.shape[0], 4), np.float64)
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_hip_debug_pit2d(device, pit.shape[0], pit.ctypes.data_as(_P), out.ctypes.data_as(_P), err, 512)
+    if rc != OK:
+        _raise(rc, err)
+    return out

@@ -1,0 +1,141 @@
+// geom.hpp -- geometry for the gfx950 SDF kernels (and the native CPU backend).
+//
+// Bit-exact restatement of the reference's CPU arithmetic:
+//   point_segment_distance  cpu_lib/makelevelset3.cpp:21-34
+//   point_triangle_distance cpu_lib/makelevelset3.cpp:49-70
+//   orientation             cpu_lib/makelevelset3.cpp:155-165
+//   point_in_triangle_2d    cpu_lib/makelevelset3.cpp:169-187
+// with the evaluation order of common/vec.h (mag2 :216-222, dist :239-255,
+// dot :377-383, scalar*Vec :331-337) and std::min/max of common/util.h:22-23.
+// Every translation unit including this file is compiled -ffp-contract=off
+// (the CPU oracle has no FMA), float '/' and sqrt are the IEEE
+// correctly-rounded forms, and min/max are written as the std:: selects
+// ((b<a)?b:a), never v_min_f32, whose NaN rule differs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// The same functions serve the device kernels and the library's native CPU backend
+// (cpu_backend.cpp, host code of the same hipcc build): SDF_HD marks them for both.
+#define SDF_HD __host__ __device__ __forceinline__
+
+namespace sdfhip {
+
+// IEEE correctly-rounded float sqrt and division on both sides.
+SDF_HD float sqrt_rn(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __fsqrt_rn(x);
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+SDF_HD float div_rn(float a, float b)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __fdiv_rn(a, b);
+#else
+    return a / b;
+#endif
+}
+
+struct f3 {
+    float x, y, z;
+};
+
+SDF_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+SDF_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+SDF_HD f3 mk3(float x, float y, float z) { return f3{x, y, z}; }
+SDF_HD f3 sub3(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+SDF_HD float mag2(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+SDF_HD float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+SDF_HD float fmin_std(float a, float b) { return (b < a) ? b : a; }
+SDF_HD float fmax_std(float a, float b) { return (a < b) ? b : a; }
+SDF_HD double dmin_std(double a, double b) { return (b < a) ? b : a; }
+SDF_HD double dmax_std(double a, double b) { return (a < b) ? b : a; }
+SDF_HD double dmin3(double a, double b, double c) { return dmin_std(a, dmin_std(b, c)); }
+SDF_HD double dmax3(double a, double b, double c) { return dmax_std(a, dmax_std(b, c)); }
+SDF_HD int clampi(int a, int lo, int hi) { return (a < lo) ? lo : ((a > hi) ? hi : a); }
+
+// C++ int(double) as compiled for x86-64 (cvttsd2si): truncation toward zero,
+// INT_MIN when out of range or NaN.  (v_cvt_i32_f64 would saturate instead.)
+SDF_HD int trunc_to_int(double v)
+{
+    return (v > -2147483649.0 && v < 2147483648.0) ? (int)v : (int)0x80000000;
+}
+SDF_HD int wrap_add(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
+
+SDF_HD float dist3(f3 a, f3 b)
+{
+    f3 d = sub3(a, b);
+    return sqrt_rn((d.x * d.x + d.y * d.y) + d.z * d.z);
+}
+
+// point_segment_distance.  The reference divides in FP64: (float)((double)dot / (double)m2).
+SDF_HD float psd(f3 x0, f3 x1, f3 x2)
+{
+    f3 e = sub3(x2, x1);
+    double m2 = (double)mag2(e);
+    f3 t = sub3(x2, x0);
+    float s12 = (float)((double)dot3(t, e) / m2);
+    if (s12 < 0.0f) s12 = 0.0f;
+    else if (s12 > 1.0f) s12 = 1.0f;
+    float w = 1.0f - s12;
+    f3 p = mk3(x1.x * s12 + x2.x * w, x1.y * s12 + x2.y * w, x1.z * s12 + x2.z * w);
+    return dist3(x0, p);
+}
+
+// point_triangle_distance.
+SDF_HD float ptd(f3 x0, f3 x1, f3 x2, f3 x3)
+{
+    f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3), x03 = sub3(x0, x3);
+    float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
+    float invdet = div_rn(1.0f, fmax_std(m13 * m23 - d * d, 1e-30f));
+    float a = dot3(x13, x03), b = dot3(x23, x03);
+    float w23 = invdet * (m23 * a - d * b);
+    float w31 = invdet * (m13 * b - d * a);
+    float w12 = (1.0f - w23) - w31;
+    if (w23 >= 0.0f && w31 >= 0.0f && w12 >= 0.0f) {
+        f3 p = mk3((x1.x * w23 + x2.x * w31) + x3.x * w12,
+                   (x1.y * w23 + x2.y * w31) + x3.y * w12,
+                   (x1.z * w23 + x2.z * w31) + x3.z * w12);
+        return dist3(x0, p);
+    }
+    if (w23 > 0.0f) return fmin_std(psd(x0, x1, x2), psd(x0, x1, x3));
+    if (w31 > 0.0f) return fmin_std(psd(x0, x1, x2), psd(x0, x2, x3));
+    return fmin_std(psd(x0, x1, x3), psd(x0, x2, x3));
+}
+
+// orientation (SOS-robust 2D), FP64.
+SDF_HD int orientation(double x1, double y1, double x2, double y2, double &area)
+{
+    area = y1 * x2 - x1 * y2;
+    if (area > 0) return 1;
+    if (area < 0) return -1;
+    if (y2 > y1) return 1;
+    if (y2 < y1) return -1;
+    if (x1 > x2) return 1;
+    if (x1 < x2) return -1;
+    return 0;
+}
+
+SDF_HD bool pit2d(double x0, double y0, double x1, double y1, double x2, double y2,
+                                      double x3, double y3, double &a, double &b, double &c)
+{
+    x1 -= x0; x2 -= x0; x3 -= x0;
+    y1 -= y0; y2 -= y0; y3 -= y0;
+    int sa = orientation(x2, y2, x3, y3, a);
+    if (sa == 0) return false;
+    int sb = orientation(x3, y3, x1, y1, b);
+    if (sb != sa) return false;
+    int sc = orientation(x1, y1, x2, y2, c);
+    if (sc != sa) return false;
+    double sum = (a + b) + c;
+    a /= sum;
+    b /= sum;
+    c /= sum;
+    return true;
+}
+
+}  // namespace sdfhip

@@ -1,0 +1,620 @@
+// sdfgen_hip.hip -- MI355X (gfx950) backend for make_level_set3 behind the C-ABI in
+// include/sdfgen_hip.h.
+//
+// Pipeline (one HIP stream per call):
+//   k_prep   : gather the indexed mesh into a per-triangle vertex soup (48 B/tri),
+//              validate indices, initialise the cell state         (:196-199)
+//   k_band   : one wave per triangle -- exact distances over the band box with a
+//              packed u64 atomicMin key (f32bits(d)<<32 | t) that reproduces the
+//              CPU's ascending-t strict-< rule, and ray-parity counts (:203-236)
+//   sweeps   : 2 passes x 8 directions of the Gauss-Seidel sweep (:238-292),
+//              reproduced bit-exactly by a hyperplane-ordered wavefront
+//   k_sign   : one wave per (j,k) row -- ballot prefix parity, sign flip, output in
+//              the caller's layout (:294-303)
+// Cell state is one u64 per cell: high word = phi bits, low word = closest_tri.
+// Line references are to /root/reference/cpu_lib/makelevelset3.cpp unless noted.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "geom.hpp"
+#include "sdfgen_hip.h"
+#include "sweep_wavefront.hpp"
+
+using namespace sdfhip;
+
+namespace {
+
+typedef unsigned long long u64;
+
+// ---------------------------------------------------------------------------
+// error plumbing
+// ---------------------------------------------------------------------------
+struct Err {
+    char *buf;
+    size_t len;
+    int set(int code, const char *fmt, ...)
+    {
+        if (buf && len) {
+            va_list ap;
+            va_start(ap, fmt);
+            vsnprintf(buf, len, fmt, ap);
+            va_end(ap);
+        }
+        return code;
+    }
+};
+
+#define HIPCHK(expr)                                                                            \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return err.set(e_ == hipErrorOutOfMemory ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, \
+                           "GPU (HIP) error %s at %s:%d: %s", hipGetErrorName(e_), __FILE__,    \
+                           __LINE__, #expr);                                                    \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+
+// Gather the indexed mesh into 3 float4 per triangle; validate indices; init cells.
+__global__ void k_prep_soup(const uint32_t *__restrict__ tri, uint64_t ntri, const float *__restrict__ xyz,
+                            uint64_t nvert, float4 *__restrict__ soup, int *__restrict__ err_flag)
+{
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < ntri;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t v[3] = {tri[3 * t + 0], tri[3 * t + 1], tri[3 * t + 2]};
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            uint64_t q = v[c];
+            if (q >= nvert) {
+                atomicOr(err_flag, 1);
+                q = 0;
+            }
+            soup[3 * t + c] = make_float4(xyz[3 * q + 0], xyz[3 * q + 1], xyz[3 * q + 2], 0.0f);
+        }
+    }
+}
+
+__global__ void k_init(u64 *__restrict__ cell, uint32_t *__restrict__ cnt, uint64_t n, u64 init_key)
+{
+    for (uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; q < n; q += (uint64_t)gridDim.x * blockDim.x) {
+        cell[q] = init_key;
+        cnt[q] = 0u;
+    }
+}
+
+struct Grid {
+    float ox, oy, oz, dx;
+    int ni, nj, nk;
+};
+
+__device__ __forceinline__ f3 load_vtx(const float4 *soup, uint64_t t, int c)
+{
+    float4 v = soup[3 * t + c];
+    return mk3(v.x, v.y, v.z);
+}
+
+__device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
+{
+    return (size_t)i + (size_t)ni * ((size_t)j + (size_t)nj * (size_t)k);
+}
+
+// Narrow band + ray parity, one 64-lane wave per triangle (grid-stride over triangles).
+//   :206-220 band, :222-235 parity
+__global__ void __launch_bounds__(256) k_band(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
+                                              float init, u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
+                                              unsigned long long *__restrict__ eval_count)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long evals = 0;
+    for (uint64_t t = wave; t < ntri; t += nwaves) {
+        f3 xp = load_vtx(soup, t, 0), xq = load_vtx(soup, t, 1), xr = load_vtx(soup, t, 2);
+        const double ox = g.ox, oy = g.oy, oz = g.oz, ddx = g.dx;
+        double fip = ((double)xp.x - ox) / ddx, fjp = ((double)xp.y - oy) / ddx, fkp = ((double)xp.z - oz) / ddx;
+        double fiq = ((double)xq.x - ox) / ddx, fjq = ((double)xq.y - oy) / ddx, fkq = ((double)xq.z - oz) / ddx;
+        double fir = ((double)xr.x - ox) / ddx, fjr = ((double)xr.y - oy) / ddx, fkr = ((double)xr.z - oz) / ddx;
+        int i0 = clampi(wrap_add(trunc_to_int(dmin3(fip, fiq, fir)), -band), 0, g.ni - 1);
+        int i1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fip, fiq, fir)), band), 1), 0, g.ni - 1);
+        int j0 = clampi(wrap_add(trunc_to_int(dmin3(fjp, fjq, fjr)), -band), 0, g.nj - 1);
+        int j1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fjp, fjq, fjr)), band), 1), 0, g.nj - 1);
+        int k0 = clampi(wrap_add(trunc_to_int(dmin3(fkp, fkq, fkr)), -band), 0, g.nk - 1);
+        int k1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fkp, fkq, fkr)), band), 1), 0, g.nk - 1);
+        if (i1 >= i0 && j1 >= j0 && k1 >= k0) {
+            const uint32_t bi = (uint32_t)(i1 - i0 + 1), bj = (uint32_t)(j1 - j0 + 1);
+            const uint64_t bij = (uint64_t)bi * bj;
+            const uint64_t total = bij * (uint64_t)(k1 - k0 + 1);
+            evals += total;
+            for (uint64_t c = lane; c < total; c += 64) {
+                const uint32_t kk = (uint32_t)(c / bij);
+                const uint32_t rem = (uint32_t)(c - (uint64_t)kk * bij);
+                const uint32_t jj = rem / bi;
+                const int i = i0 + (int)(rem - jj * bi), j = j0 + (int)jj, k = k0 + (int)kk;
+                f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
+                float d = ptd(gx, xp, xq, xr);
+                if (d < init) {  // also rejects NaN
+                    u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
+                    u64 *p = cell + cidx(i, j, k, g.ni, g.nj);
+                    if (key < *p) atomicMin(p, key);
+                }
+            }
+        }
+        // ray-parity counts
+        int pj0 = clampi(trunc_to_int(ceil(dmin3(fjp, fjq, fjr))), 0, g.nj - 1);
+        int pj1 = clampi(trunc_to_int(floor(dmax3(fjp, fjq, fjr))), 0, g.nj - 1);
+        int pk0 = clampi(trunc_to_int(ceil(dmin3(fkp, fkq, fkr))), 0, g.nk - 1);
+        int pk1 = clampi(trunc_to_int(floor(dmax3(fkp, fkq, fkr))), 0, g.nk - 1);
+        if (pj1 >= pj0 && pk1 >= pk0) {
+            const uint32_t bj = (uint32_t)(pj1 - pj0 + 1);
+            const uint64_t total = (uint64_t)bj * (uint64_t)(pk1 - pk0 + 1);
+            for (uint64_t c = lane; c < total; c += 64) {
+                const uint32_t kk = (uint32_t)(c / bj);
+                const int j = pj0 + (int)(c - (uint64_t)kk * bj), k = pk0 + (int)kk;
+                double a, b, cc;
+                if (pit2d((double)j, (double)k, fjp, fkp, fjq, fkq, fjr, fkr, a, b, cc)) {
+                    double fi = (a * fip + b * fiq) + cc * fir;
+                    int ii = trunc_to_int(ceil(fi));
+                    if (ii < 0) atomicAdd(cnt + cidx(0, j, k, g.ni, g.nj), 1u);
+                    else if (ii < g.ni) atomicAdd(cnt + cidx(ii, j, k, g.ni, g.nj), 1u);
+                }
+            }
+        }
+    }
+    if (eval_count && lane == 0 && evals) atomicAdd(eval_count, evals);
+}
+
+// One sweep cell update: the CPU's sequential check_neighbour chain (:90-102, :143-149)
+// with the exact skips (a candidate equal to the cell's own original label, or to an
+// earlier candidate's label, evaluates to the same float and can never pass strict <).
+__device__ __forceinline__ void sweep_cell(const float4 *__restrict__ soup, u64 *__restrict__ cell, const Grid &g,
+                                           int i, int j, int k, int di, int dj, int dk)
+{
+    const size_t c0 = cidx(i, j, k, g.ni, g.nj);
+    const u64 own = cell[c0];
+    float phi = __uint_as_float((uint32_t)(own >> 32));
+    int32_t ct = (int32_t)(uint32_t)own;
+    const int32_t ct_orig = ct;
+    int32_t nb[7];
+    nb[0] = (int32_t)(uint32_t)cell[cidx(i - di, j, k, g.ni, g.nj)];
+    nb[1] = (int32_t)(uint32_t)cell[cidx(i, j - dj, k, g.ni, g.nj)];
+    nb[2] = (int32_t)(uint32_t)cell[cidx(i - di, j - dj, k, g.ni, g.nj)];
+    nb[3] = (int32_t)(uint32_t)cell[cidx(i, j, k - dk, g.ni, g.nj)];
+    nb[4] = (int32_t)(uint32_t)cell[cidx(i - di, j, k - dk, g.ni, g.nj)];
+    nb[5] = (int32_t)(uint32_t)cell[cidx(i, j - dj, k - dk, g.ni, g.nj)];
+    nb[6] = (int32_t)(uint32_t)cell[cidx(i - di, j - dj, k - dk, g.ni, g.nj)];
+    const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
+    bool changed = false;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const int32_t t = nb[q];
+        bool skip = (t < 0) || (t == ct_orig);
+#pragma unroll
+        for (int r = 0; r < q; ++r) skip = skip || (nb[r] == t);
+        if (!skip) {
+            float d = ptd(gx, load_vtx(soup, (uint64_t)t, 0), load_vtx(soup, (uint64_t)t, 1),
+                          load_vtx(soup, (uint64_t)t, 2));
+            if (d < phi) {
+                phi = d;
+                ct = t;
+                changed = true;
+            }
+        }
+    }
+    if (changed) cell[c0] = ((u64)__float_as_uint(phi) << 32) | (u64)(uint32_t)ct;
+}
+
+// Reference-order sweep, one launch per oriented hyperplane s = a+b+c:
+// every upwind neighbour of a cell lies on hyperplane s-1..s-3, finished by earlier launches.
+__global__ void __launch_bounds__(256) k_sweep_plane(const float4 *__restrict__ soup, u64 *__restrict__ cell, Grid g,
+                                                     int di, int dj, int dk, int s, int a_lo, int b_lo, int b_cnt,
+                                                     int n_threads)
+{
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n_threads) return;
+    const int a = a_lo + idx / b_cnt;
+    const int b = b_lo + idx % b_cnt;
+    const int c = s - a - b;
+    if (c < 0 || c >= g.nk - 1) return;
+    if (b >= g.nj - 1) return;
+    const int i = di > 0 ? a + 1 : g.ni - 2 - a;
+    const int j = dj > 0 ? b + 1 : g.nj - 2 - b;
+    const int k = dk > 0 ? c + 1 : g.nk - 2 - c;
+    sweep_cell(soup, cell, g, i, j, k, di, dj, dk);
+}
+
+// Sign pass: one wave per (j,k) row; prefix parity by ballot, sign flip (-0.0 kept),
+// output in Array3f (i-fastest) or k-fastest layout.   :294-303
+__global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, const uint32_t *__restrict__ cnt, Grid g,
+                                              int layout, float *__restrict__ out)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t row = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nrows = (uint64_t)g.nj * g.nk;
+    if (row >= nrows) return;
+    const int j = (int)(row % g.nj), k = (int)(row / g.nj);
+    const size_t base = cidx(0, j, k, g.ni, g.nj);
+    uint32_t carry = 0;
+    for (int i0 = 0; i0 < g.ni; i0 += 64) {
+        const int i = i0 + lane;
+        const bool ok = i < g.ni;
+        uint32_t par = ok ? (cnt[base + i] & 1u) : 0u;
+        const u64 mask = __ballot(par);
+        const u64 below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);  // lanes 0..lane
+        const uint32_t pre = (carry + (uint32_t)__popcll(mask & below)) & 1u;
+        if (ok) {
+            uint32_t bits = (uint32_t)(cell[base + i] >> 32);
+            if (pre) bits ^= 0x80000000u;
+            float v = __uint_as_float(bits);
+            if (layout == SDFGEN_LAYOUT_ARRAY3) out[base + i] = v;
+            else out[((size_t)i * g.nj + j) * g.nk + k] = v;
+        }
+        carry = (carry + (uint32_t)__popcll(mask)) & 1u;
+    }
+}
+
+// Diagnostics kernels.
+__global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__restrict__ out)
+{
+    uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const float *p = pts + 12 * q;
+    out[q] = ptd(mk3(p[0], p[1], p[2]), mk3(p[3], p[4], p[5]), mk3(p[6], p[7], p[8]), mk3(p[9], p[10], p[11]));
+}
+
+__global__ void k_debug_pit2d(uint64_t n, const double *__restrict__ in, double *__restrict__ out)
+{
+    uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    const double *p = in + 8 * q;
+    double a = 0, b = 0, c = 0;
+    bool r = pit2d(p[0], p[1], p[2], p[3], p[4], p[5], p[6], p[7], a, b, c);
+    out[4 * q] = r ? 1.0 : 0.0;
+    out[4 * q + 1] = a;
+    out[4 * q + 2] = b;
+    out[4 * q + 3] = c;
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+const int SWEEP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
+                              {+1, -1, +1}, {-1, +1, -1}, {+1, -1, -1}, {-1, +1, +1}};
+
+struct Workspace {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    u64 *cell = nullptr;
+    uint32_t *cnt = nullptr;
+    float4 *soup = nullptr;
+    uint32_t *tri = nullptr;
+    float *xyz = nullptr;
+    int *err_flag = nullptr;
+    unsigned long long *evals = nullptr;
+    size_t cap_cell = 0, cap_cnt = 0, cap_soup = 0, cap_tri = 0, cap_xyz = 0;
+    hipEvent_t ev[40] = {};
+    bool ev_ok = false;
+    std::mutex mu;
+    WavefrontWorkspace wf;
+};
+
+std::mutex g_mu;
+std::vector<Workspace *> g_ws;
+sdfgen_hip_profile g_prof;
+std::mutex g_prof_mu;
+
+template <class T>
+int grow(T **p, size_t *cap, size_t need, Err &err)
+{
+    if (need <= *cap && *p) return 0;
+    if (*p) {
+        HIPCHK(hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+    }
+    size_t n = std::max<size_t>(need, 1);
+    HIPCHK(hipMalloc((void **)p, n * sizeof(T)));
+    *cap = n;
+    return 0;
+}
+
+int get_ws(int device, Workspace **out, Err &err)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (Workspace *w : g_ws)
+        if (w->device == device) {
+            *out = w;
+            return 0;
+        }
+    Workspace *w = new Workspace();
+    w->device = device;
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking));
+    for (auto &e : w->ev) HIPCHK(hipEventCreate(&e));
+    w->ev_ok = true;
+    g_ws.push_back(w);
+    *out = w;
+    return 0;
+}
+
+int validate(uint64_t ntri, uint64_t nvert, float dx, int ni, int nj, int nk, int layout, Err &err)
+{
+    if (ni <= 0 || nj <= 0 || nk <= 0)
+        return err.set(SDFGEN_HIP_EINVAL, "Grid dimensions must be positive (nx, ny, nz > 0)");
+    if (!(dx > 0.0f) || !std::isfinite(dx)) return err.set(SDFGEN_HIP_EINVAL, "Cell spacing dx must be positive");
+    if (layout != SDFGEN_LAYOUT_ARRAY3 && layout != SDFGEN_LAYOUT_KFAST)
+        return err.set(SDFGEN_HIP_EINVAL, "out_layout must be 0 (Array3f) or 1 (k-fastest)");
+    if ((uint64_t)ni * nj * nk >= (1ull << 40)) return err.set(SDFGEN_HIP_EINVAL, "grid too large");
+    if (ntri > 0x7fffffffull) return err.set(SDFGEN_HIP_EINVAL, "too many triangles (> 2^31-1)");
+    (void)nvert;
+    return 0;
+}
+
+inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap)
+{
+    uint64_t b = (n + block - 1) / block;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
+// The whole pipeline on device buffers already resident on ws->device.
+int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
+                 uint64_t nvert, const float origin[3], float dx, int ni, int nj, int nk, int band, int layout,
+                 float *d_out, Err &err)
+{
+    const uint64_t n = (uint64_t)ni * nj * nk;
+    int rc;
+    if ((rc = grow(&ws->cell, &ws->cap_cell, n, err))) return rc;
+    if ((rc = grow(&ws->cnt, &ws->cap_cnt, n, err))) return rc;
+    if ((rc = grow(&ws->soup, &ws->cap_soup, 3 * std::max<uint64_t>(ntri, 1), err))) return rc;
+    if (!ws->err_flag) {
+        HIPCHK(hipMalloc((void **)&ws->err_flag, sizeof(int)));
+        HIPCHK(hipMalloc((void **)&ws->evals, sizeof(unsigned long long)));
+    }
+    Grid g{origin[0], origin[1], origin[2], dx, ni, nj, nk};
+    const float init = (float)(ni + nj + nk) * dx;  // :197
+    const u64 init_key = ((u64)__builtin_bit_cast(uint32_t, init) << 32) | 0xffffffffull;
+
+    hipEvent_t *ev = ws->ev;
+    HIPCHK(hipEventRecord(ev[0], st));
+    HIPCHK(hipMemsetAsync(ws->err_flag, 0, sizeof(int), st));
+    HIPCHK(hipMemsetAsync(ws->evals, 0, sizeof(unsigned long long), st));
+    if (ntri) {
+        hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, d_tri, ntri, d_xyz, nvert,
+                           ws->soup, ws->err_flag);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, ws->cell, ws->cnt, n, init_key);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev[1], st));
+    if (ntri) {
+        hipLaunchKernelGGL(k_band, dim3(grid_for(ntri * 64, 256, 65536)), dim3(256), 0, st, ws->soup, ntri, g, band,
+                           init, ws->cell, ws->cnt, ws->evals);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[2], st));
+
+    // ---- sweeps ----
+    int launches = 0;
+    const int A = ni - 1, B = nj - 1, C = nk - 1;
+    const bool do_sweep = (A > 0 && B > 0 && C > 0 && ntri > 0);
+    int impl = 0;
+    if (do_sweep && wavefront_supported(ni, nj, nk)) impl = 1;
+    for (int s = 0; s < 16; ++s) {
+        HIPCHK(hipEventRecord(ev[3 + s], st));
+        if (!do_sweep) continue;
+        const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
+        if (impl == 1) {
+            if ((rc = wavefront_sweep(ws->wf, st, ws->soup, ws->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
+                                      err.len)))
+                return rc;
+            ++launches;
+            continue;
+        }
+        for (int h = 0; h <= A + B + C - 3; ++h) {
+            const int a_lo = std::max(0, h - (B - 1) - (C - 1)), a_hi = std::min(A - 1, h);
+            const int b_lo = std::max(0, h - (A - 1) - (C - 1)), b_hi = std::min(B - 1, h);
+            if (a_hi < a_lo || b_hi < b_lo) continue;
+            const int a_cnt = a_hi - a_lo + 1, b_cnt = b_hi - b_lo + 1;
+            const int nthr = a_cnt * b_cnt;
+            hipLaunchKernelGGL(k_sweep_plane, dim3((nthr + 255) / 256), dim3(256), 0, st, ws->soup, ws->cell, g, di,
+                               dj, dk, h, a_lo, b_lo, b_cnt, nthr);
+            ++launches;
+        }
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[19], st));
+    {
+        const uint64_t rows = (uint64_t)nj * nk;
+        hipLaunchKernelGGL(k_sign, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, st, ws->cell, ws->cnt, g,
+                           layout, d_out);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[20], st));
+    int flag = 0;
+    unsigned long long evals = 0;
+    HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&evals, ws->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipGetLastError());
+
+    sdfgen_hip_profile p;
+    memset(&p, 0, sizeof(p));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[20]));
+    p.total_ms = ms;
+    HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+    p.prep_ms = ms;
+    HIPCHK(hipEventElapsedTime(&ms, ev[1], ev[2]));
+    p.band_ms = ms;
+    HIPCHK(hipEventElapsedTime(&ms, ev[3], ev[19]));
+    p.sweep_ms = ms;
+    for (int s = 0; s < 16; ++s) {
+        HIPCHK(hipEventElapsedTime(&ms, ev[3 + s], ev[(s == 15) ? 19 : 4 + s]));
+        p.sweep_launch_ms[s] = ms;
+    }
+    HIPCHK(hipEventElapsedTime(&ms, ev[19], ev[20]));
+    p.sign_ms = ms;
+    p.sweep_launches = launches;
+    p.sweep_impl = impl;
+    p.band_evals = evals;
+    {
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof = p;
+    }
+    if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
+                             (unsigned long long)nvert);
+    return 0;
+}
+
+int device_count_impl()
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+}  // namespace
+
+extern "C" {
+
+int sdfgen_hip_abi_version(void) { return SDFGEN_HIP_ABI_VERSION; }
+
+int sdfgen_hip_device_count(void) { return device_count_impl(); }
+
+int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert,
+                               const float origin[3], float dx, int ni, int nj, int nk, int exact_band, int ngpu,
+                               int out_layout, float *phi_out, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    int rc = validate(ntri, nvert, dx, ni, nj, nk, out_layout, err);
+    if (rc) return rc;
+    if (!phi_out || !origin || (ntri && (!tri || !xyz)))
+        return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    const int ndev = device_count_impl();
+    if (ndev <= 0) return err.set(SDFGEN_HIP_ENODEV, "GPU backend requested but no HIP GPU device is available");
+    (void)ngpu;  // multi-device Z-slab path: see DESIGN.md (single device in this build)
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    Workspace *ws = nullptr;
+    if ((rc = get_ws(dev, &ws, err))) return rc;
+    std::lock_guard<std::mutex> lk(ws->mu);
+    HIPCHK(hipSetDevice(dev));
+    const uint64_t n = (uint64_t)ni * nj * nk;
+    if ((rc = grow(&ws->tri, &ws->cap_tri, std::max<uint64_t>(3 * ntri, 1), err))) return rc;
+    if ((rc = grow(&ws->xyz, &ws->cap_xyz, std::max<uint64_t>(3 * nvert, 1), err))) return rc;
+    float *d_out = nullptr;
+    HIPCHK(hipMalloc((void **)&d_out, n * sizeof(float)));
+    hipStream_t st = ws->stream;
+    if (ntri) {
+        HIPCHK(hipMemcpyAsync(ws->tri, tri, 3 * ntri * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ws->xyz, xyz, 3 * nvert * sizeof(float), hipMemcpyHostToDevice, st));
+    }
+    rc = run_pipeline(ws, st, ws->tri, ntri, ws->xyz, nvert, origin, dx, ni, nj, nk, exact_band, out_layout, d_out,
+                      err);
+    if (rc == 0) {
+        hipError_t e = hipMemcpyAsync(phi_out, d_out, n * sizeof(float), hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) rc = err.set(SDFGEN_HIP_ERUNTIME, "GPU (HIP) error %s copying phi", hipGetErrorName(e));
+    }
+    hipFree(d_out);
+    return rc;
+}
+
+int sdfgen_hip_make_level_set3_device(int device, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
+                                      uint64_t nvert, const float origin[3], float dx, int ni, int nj, int nk,
+                                      int exact_band, int out_layout, float *d_phi_out, void *hip_stream,
+                                      char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    int rc = validate(ntri, nvert, dx, ni, nj, nk, out_layout, err);
+    if (rc) return rc;
+    if (!d_phi_out || !origin || (ntri && (!d_tri || !d_xyz)))
+        return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    const int ndev = device_count_impl();
+    if (device < 0 || device >= ndev) return err.set(SDFGEN_HIP_ENODEV, "GPU device %d not available", device);
+    HIPCHK(hipSetDevice(device));
+    Workspace *ws = nullptr;
+    if ((rc = get_ws(device, &ws, err))) return rc;
+    std::lock_guard<std::mutex> lk(ws->mu);
+    HIPCHK(hipSetDevice(device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ws->stream;
+    return run_pipeline(ws, st, d_tri, ntri, d_xyz, nvert, origin, dx, ni, nj, nk, exact_band, out_layout, d_phi_out,
+                        err);
+}
+
+int sdfgen_hip_last_profile(sdfgen_hip_profile *out)
+{
+    if (!out) return SDFGEN_HIP_EINVAL;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    *out = g_prof;
+    return 0;
+}
+
+int sdfgen_hip_release(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (Workspace *w : g_ws) {
+        hipSetDevice(w->device);
+        hipFree(w->cell);
+        hipFree(w->cnt);
+        hipFree(w->soup);
+        hipFree(w->tri);
+        hipFree(w->xyz);
+        hipFree(w->err_flag);
+        hipFree(w->evals);
+        wavefront_release(w->wf);
+        for (auto &e : w->ev) hipEventDestroy(e);
+        hipStreamDestroy(w->stream);
+        delete w;
+    }
+    g_ws.clear();
+    return 0;
+}
+
+int sdfgen_hip_debug_ptd(int device, uint64_t n, const float *pts, float *out, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "no GPU device %d", device);
+    HIPCHK(hipSetDevice(device));
+    float *dp = nullptr, *dout = nullptr;
+    HIPCHK(hipMalloc((void **)&dp, std::max<uint64_t>(n, 1) * 12 * sizeof(float)));
+    HIPCHK(hipMalloc((void **)&dout, std::max<uint64_t>(n, 1) * sizeof(float)));
+    HIPCHK(hipMemcpy(dp, pts, n * 12 * sizeof(float), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_ptd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, dp, dout);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(out, dout, n * sizeof(float), hipMemcpyDeviceToHost));
+    hipFree(dp);
+    hipFree(dout);
+    return 0;
+}
+
+int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *out4, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "no GPU device %d", device);
+    HIPCHK(hipSetDevice(device));
+    double *dp = nullptr, *dout = nullptr;
+    HIPCHK(hipMalloc((void **)&dp, std::max<uint64_t>(n, 1) * 8 * sizeof(double)));
+    HIPCHK(hipMalloc((void **)&dout, std::max<uint64_t>(n, 1) * 4 * sizeof(double)));
+    HIPCHK(hipMemcpy(dp, pit, n * 8 * sizeof(double), hipMemcpyHostToDevice));
+    hipLaunchKernelGGL(k_debug_pit2d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, dp, dout);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy(out4, dout, n * 4 * sizeof(double), hipMemcpyDeviceToHost));
+    hipFree(dp);
+    hipFree(dout);
+    return 0;
+}
+
+}  // extern "C"
