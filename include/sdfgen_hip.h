@@ -97,7 +97,8 @@ typedef struct sdfgen_hip_profile {
     int sweep_launches;       /* kernel launches issued for the sweeps */
     int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined column wavefront */
     uint64_t band_evals;      /* point-triangle evaluations in the band phase */
-    uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless counting enabled) */
+    uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless SDFGEN_COUNT_EVALS is set) */
+    uint64_t sweep_stalls;    /* workgroup iterations spent waiting for halo hand-offs (same) */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

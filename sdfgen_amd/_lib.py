@@ -48,6 +48,7 @@ class Profile(ctypes.Structure):
         ("sweep_impl", ctypes.c_int),
         ("band_evals", ctypes.c_uint64),
         ("sweep_evals", ctypes.c_uint64),
+        ("sweep_stalls", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -21,23 +21,12 @@
 
 namespace sdfhip {
 
-// IEEE correctly-rounded float sqrt and division on both sides.
-SDF_HD float sqrt_rn(float x)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __fsqrt_rn(x);
-#else
-    return __builtin_sqrtf(x);
-#endif
-}
-SDF_HD float div_rn(float a, float b)
-{
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __fdiv_rn(a, b);
-#else
-    return a / b;
-#endif
-}
+// IEEE correctly-rounded float sqrt and division on both sides.  NOTE: on ROCm 7.2
+// __fsqrt_rn() lowers to a bare v_sqrt_f32 (1 ulp, NOT correctly rounded); the
+// plain builtin gets the v_sqrt + two-FMA-residual fix-up that is.  Plain '/' gets
+// the v_div_scale/v_div_fmas/v_div_fixup IEEE sequence.
+SDF_HD float sqrt_rn(float x) { return __builtin_sqrtf(x); }
+SDF_HD float div_rn(float a, float b) { return a / b; }
 
 struct f3 {
     float x, y, z;

@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -409,6 +410,12 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     const bool do_sweep = (A > 0 && B > 0 && C > 0 && ntri > 0);
     int impl = 0;
     if (do_sweep && wavefront_supported(ni, nj, nk)) impl = 1;
+    {
+        const char *e = getenv("SDFGEN_SWEEP");  // diagnostics: "plane" forces the hyperplane launches
+        if (e && strcmp(e, "plane") == 0) impl = 0;
+        ws->wf.count_evals = getenv("SDFGEN_COUNT_EVALS") != nullptr;
+        if (ws->wf.count_evals && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 16, st));
+    }
     for (int s = 0; s < 16; ++s) {
         HIPCHK(hipEventRecord(ev[3 + s], st));
         if (!do_sweep) continue;
@@ -440,9 +447,13 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[20], st));
-    int flag = 0;
-    unsigned long long evals = 0;
+    int flag = 0, wf_err = 0;
+    unsigned long long evals = 0, wf_stats[2] = {0, 0};
     HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (impl == 1) {
+        HIPCHK(hipMemcpyAsync(&wf_err, ws->wf.ctrl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
+        if (ws->wf.count_evals) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, 16, hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(hipMemcpyAsync(&evals, ws->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipGetLastError());
@@ -467,10 +478,13 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sweep_launches = launches;
     p.sweep_impl = impl;
     p.band_evals = evals;
+    p.sweep_evals = wf_stats[0];
+    p.sweep_stalls = wf_stats[1];
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;
     }
+    if (wf_err) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
                              (unsigned long long)nvert);
     return 0;

@@ -159,3 +159,23 @@ def test_gpu_device_entry_with_torch_buffers():
     assert bits_equal(got, want), diff_report(got, want, dx)
     prof = _lib.last_profile()
     assert prof["total_ms"] > 0 and prof["band_evals"] > 0
+
+
+# ---------------------------------------------------------------- both sweep implementations
+@pytest.fixture(params=["plane", "wavefront"])
+def sweep_impl(request, monkeypatch):
+    if request.param == "plane":
+        monkeypatch.setenv("SDFGEN_SWEEP", "plane")
+    else:
+        monkeypatch.delenv("SDFGEN_SWEEP", raising=False)
+    return request.param
+
+
+@pytest.mark.parametrize("nu,nv,dims", [(90, 31, (57, 33, 70)), (40, 21, (17, 40, 35)), (200, 61, (64, 48, 40))])
+def test_gpu_sweep_impls_agree_with_oracle(sweep_impl, nu, nv, dims):
+    v, t = meshgen.bumpy_sphere(nu, nv)
+    o, dx = meshgen.grid_mode2b(v, *dims, 2)
+    want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, *dims, exact_band=1))
+    got = _lib.make_level_set3(v, t, o, dx, *dims, 1)
+    assert _lib.last_profile()["sweep_impl"] == (0 if sweep_impl == "plane" else 1)
+    assert bits_equal(got, want), diff_report(got, want, dx)
