@@ -95,10 +95,11 @@ typedef struct sdfgen_hip_profile {
     double sign_ms;           /* sign pass + output layout */
     double sweep_launch_ms[16];  /* per (pass, direction) sweep */
     int sweep_launches;       /* kernel launches issued for the sweeps */
-    int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined column wavefront */
+    int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined 8x8-tile column wavefront */
     uint64_t band_evals;      /* point-triangle evaluations in the band phase */
     uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless SDFGEN_COUNT_EVALS is set) */
-    uint64_t sweep_stalls;    /* workgroup iterations spent waiting for halo hand-offs (same) */
+    uint64_t sweep_stalls;    /* compute-wave polls that found a hand-off not yet landed (same) */
+    uint64_t helper_polls;    /* helper-wave polls that found nothing to fetch (same) */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
@@ -107,9 +108,11 @@ int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
 int sdfgen_hip_release(void);
 
 /* Diagnostics (used by the parity tests): evaluate the device geometry kernels
- * on host arrays.  pts: n x 12 floats (x0,x1,x2,x3) -> out: n floats.
+ * on host arrays.  pts: n x 12 floats (x0,x1,x2,x3) -> out: n floats;
+ * variant 0 = point_triangle_distance as used by the band kernel, 1 = the
+ * branch-free form used by the sweep kernel (must give identical bits).
  * pit: n x 8 doubles (x0,y0,x1,y1,x2,y2,x3,y3) -> out4: n x (flag,a,b,c). */
-int sdfgen_hip_debug_ptd(int device, uint64_t n, const float *pts, float *out,
+int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, float *out,
                          char *errbuf, size_t errlen);
 int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *out4,
                            char *errbuf, size_t errlen);

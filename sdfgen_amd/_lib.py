@@ -49,6 +49,7 @@ class Profile(ctypes.Structure):
         ("band_evals", ctypes.c_uint64),
         ("sweep_evals", ctypes.c_uint64),
         ("sweep_stalls", ctypes.c_uint64),
+        ("helper_polls", ctypes.c_uint64),
     ]
 
     def as_dict(self):
@@ -80,7 +81,7 @@ def _load():
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
                                              ctypes.c_char_p, ctypes.c_size_t]
     L.sdfgen_cpu_make_level_set3.restype = ctypes.c_int
-    L.sdfgen_hip_debug_ptd.argtypes = [ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_hip_debug_ptd.argtypes = [ctypes.c_int, ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
     L.sdfgen_hip_debug_ptd.restype = ctypes.c_int
     L.sdfgen_hip_debug_pit2d.argtypes = [ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
     L.sdfgen_hip_debug_pit2d.restype = ctypes.c_int
@@ -176,11 +177,12 @@ def release() -> None:
     lib.sdfgen_hip_release()
 
 
-def debug_ptd(pts: np.ndarray, device: int = 0) -> np.ndarray:
+def debug_ptd(pts: np.ndarray, device: int = 0, variant: int = 0) -> np.ndarray:
     pts = np.ascontiguousarray(pts, dtype=np.float32).reshape(-1, 12)
     out = np.empty(pts.shape[0], np.float32)
     err = ctypes.create_string_buffer(512)
-    rc = lib.sdfgen_hip_debug_ptd(device, pts.shape[0], pts.ctypes.data_as(_P), out.ctypes.data_as(_P), err, 512)
+    rc = lib.sdfgen_hip_debug_ptd(device, variant, pts.shape[0], pts.ctypes.data_as(_P), out.ctypes.data_as(_P),
+                                  err, 512)
     if rc != OK:
         _raise(rc, err)
     return out

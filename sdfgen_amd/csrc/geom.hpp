@@ -96,6 +96,37 @@ SDF_HD float ptd(f3 x0, f3 x1, f3 x2, f3 x3)
     return fmin_std(psd(x0, x1, x3), psd(x0, x2, x3));
 }
 
+// point_triangle_distance with no divergent branches (for wave-wide evaluation on
+// the GPU).  Bit-identical to ptd(): every case performs the same operations on the
+// same operands, and min(first, second) keeps the reference's argument order
+// (cpu_lib/makelevelset3.cpp:63-68), which matters for NaN:
+//   w23 > 0 : min(psd(x1,x2), psd(x1,x3))
+//   w31 > 0 : min(psd(x1,x2), psd(x2,x3))
+//   else    : min(psd(x1,x3), psd(x2,x3))
+SDF_HD float ptd_nb(f3 x0, f3 x1, f3 x2, f3 x3)
+{
+    f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3), x03 = sub3(x0, x3);
+    float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
+    float invdet = div_rn(1.0f, fmax_std(m13 * m23 - d * d, 1e-30f));
+    float a = dot3(x13, x03), b = dot3(x23, x03);
+    float w23 = invdet * (m23 * a - d * b);
+    float w31 = invdet * (m13 * b - d * a);
+    float w12 = (1.0f - w23) - w31;
+    const bool inside = (w23 >= 0.0f && w31 >= 0.0f && w12 >= 0.0f);
+    f3 p = mk3((x1.x * w23 + x2.x * w31) + x3.x * w12,
+               (x1.y * w23 + x2.y * w31) + x3.y * w12,
+               (x1.z * w23 + x2.z * w31) + x3.z * w12);
+    const float d_in = dist3(x0, p);
+    const bool c23 = w23 > 0.0f, c31 = !c23 && (w31 > 0.0f);
+    const f3 fa = x1;                         // first segment (fa, fb)
+    const f3 fb = (c23 || c31) ? x2 : x3;
+    const f3 sa = (c23) ? x1 : x2;            // second segment (sa, x3)
+    const float first = psd(x0, fa, fb);
+    const float second = psd(x0, sa, x3);
+    const float d_edge = fmin_std(first, second);
+    return inside ? d_in : d_edge;
+}
+
 // orientation (SOS-robust 2D), FP64.
 SDF_HD int orientation(double x1, double y1, double x2, double y2, double &area)
 {

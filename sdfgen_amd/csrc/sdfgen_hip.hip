@@ -26,7 +26,7 @@
 
 #include "geom.hpp"
 #include "sdfgen_hip.h"
-#include "sweep_wavefront.hpp"
+#include "sweep_tile.hpp"
 
 using namespace sdfhip;
 
@@ -263,12 +263,14 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
 }
 
 // Diagnostics kernels.
-__global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__restrict__ out)
+__global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__restrict__ out, int variant)
 {
     uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     if (q >= n) return;
     const float *p = pts + 12 * q;
-    out[q] = ptd(mk3(p[0], p[1], p[2]), mk3(p[3], p[4], p[5]), mk3(p[6], p[7], p[8]), mk3(p[9], p[10], p[11]));
+    const f3 x0 = mk3(p[0], p[1], p[2]), x1 = mk3(p[3], p[4], p[5]), x2 = mk3(p[6], p[7], p[8]),
+             x3 = mk3(p[9], p[10], p[11]);
+    out[q] = variant == 0 ? ptd(x0, x1, x2, x3) : ptd_nb(x0, x1, x2, x3);
 }
 
 __global__ void k_debug_pit2d(uint64_t n, const double *__restrict__ in, double *__restrict__ out)
@@ -304,7 +306,7 @@ struct Workspace {
     hipEvent_t ev[40] = {};
     bool ev_ok = false;
     std::mutex mu;
-    WavefrontWorkspace wf;
+    TileSweepWorkspace wf;
 };
 
 std::mutex g_mu;
@@ -409,19 +411,19 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     const int A = ni - 1, B = nj - 1, C = nk - 1;
     const bool do_sweep = (A > 0 && B > 0 && C > 0 && ntri > 0);
     int impl = 0;
-    if (do_sweep && wavefront_supported(ni, nj, nk)) impl = 1;
+    if (do_sweep && tile_sweep_supported(ni, nj, nk)) impl = 1;
     {
         const char *e = getenv("SDFGEN_SWEEP");  // diagnostics: "plane" forces the hyperplane launches
         if (e && strcmp(e, "plane") == 0) impl = 0;
-        ws->wf.count_evals = getenv("SDFGEN_COUNT_EVALS") != nullptr;
-        if (ws->wf.count_evals && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 16, st));
+        ws->wf.count = getenv("SDFGEN_COUNT_EVALS") != nullptr;
+        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 32, st));
     }
     for (int s = 0; s < 16; ++s) {
         HIPCHK(hipEventRecord(ev[3 + s], st));
         if (!do_sweep) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
         if (impl == 1) {
-            if ((rc = wavefront_sweep(ws->wf, st, ws->soup, ws->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
+            if ((rc = tile_sweep(ws->wf, st, ws->soup, ws->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
                                       err.len)))
                 return rc;
             ++launches;
@@ -448,11 +450,11 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     }
     HIPCHK(hipEventRecord(ev[20], st));
     int flag = 0, wf_err = 0;
-    unsigned long long evals = 0, wf_stats[2] = {0, 0};
+    unsigned long long evals = 0, wf_stats[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     if (impl == 1) {
         HIPCHK(hipMemcpyAsync(&wf_err, ws->wf.ctrl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        if (ws->wf.count_evals) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, 16, hipMemcpyDeviceToHost, st));
+        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, 32, hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipMemcpyAsync(&evals, ws->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -480,6 +482,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.band_evals = evals;
     p.sweep_evals = wf_stats[0];
     p.sweep_stalls = wf_stats[1];
+    p.helper_polls = wf_stats[2];
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;
@@ -588,7 +591,7 @@ int sdfgen_hip_release(void)
         hipFree(w->xyz);
         hipFree(w->err_flag);
         hipFree(w->evals);
-        wavefront_release(w->wf);
+        tile_sweep_release(w->wf);
         for (auto &e : w->ev) hipEventDestroy(e);
         hipStreamDestroy(w->stream);
         delete w;
@@ -597,7 +600,8 @@ int sdfgen_hip_release(void)
     return 0;
 }
 
-int sdfgen_hip_debug_ptd(int device, uint64_t n, const float *pts, float *out, char *errbuf, size_t errlen)
+int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, float *out, char *errbuf,
+                         size_t errlen)
 {
     Err err{errbuf, errlen};
     if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "no GPU device %d", device);
@@ -606,7 +610,7 @@ int sdfgen_hip_debug_ptd(int device, uint64_t n, const float *pts, float *out, c
     HIPCHK(hipMalloc((void **)&dp, std::max<uint64_t>(n, 1) * 12 * sizeof(float)));
     HIPCHK(hipMalloc((void **)&dout, std::max<uint64_t>(n, 1) * sizeof(float)));
     HIPCHK(hipMemcpy(dp, pts, n * 12 * sizeof(float), hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_debug_ptd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, dp, dout);
+    hipLaunchKernelGGL(k_debug_ptd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, dp, dout, variant);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(out, dout, n * sizeof(float), hipMemcpyDeviceToHost));
     hipFree(dp);

@@ -1,0 +1,532 @@
+// sweep_tile.hpp -- one Gauss-Seidel sweep direction as ONE persistent launch:
+// a pipelined column wavefront over 8x8 (j,k) tiles, one compute wave per tile.
+//
+// Why this is exact.  The reference sweep (cpu_lib/makelevelset3.cpp:130-151)
+// visits k, then j, then i and updates each cell from its 7 upwind neighbours
+// (:143-149).  In oriented coordinates (a,b,c) (a = i-1 for di>0, ni-2-i for di<0,
+// likewise b, c) every upwind neighbour has a strictly smaller a+b+c and each cell
+// is written once per sweep, so any order that finishes a cell's upwind
+// neighbours first reproduces the sequential result bit-for-bit.
+//
+// Decomposition.  The (b,c) plane is cut into 8x8 tiles; a tile is one task for one
+// workgroup of two waves:
+//   * compute wave: lane (bl,cl) owns column (b0+bl, c0+cl) and at local step h
+//     updates cell a = h-bl-cl -- the whole tile advances one anti-diagonal per
+//     step with NO barrier: every intra-tile dependency is inside the wave, and a
+//     wave's LDS operations execute in order.  Neighbour results (label AND the
+//     triangle's vertices) live in an LDS ring, so no global load sits on the
+//     critical path.  The ~2 distinct candidates per cell (7 upwind labels minus
+//     duplicates and the cell's own label -- exact skips, see sweep_cell in
+//     sdfgen_hip.hip) are compacted across the wave (ballot + mbcnt) and evaluated
+//     two per lane with the branch-free ptd_nb, then each cell applies them in the
+//     reference's check order (strict '<', first minimum wins).
+//   * helper wave: batched, decoupled prefetch.  It streams each column's old
+//     (phi, label) and the label's vertices into an LDS "own" ring, and fills the
+//     17 halo streams (last row of tile J-1, last column of tile K-1, corner) from
+//     8-byte tagged granules {epoch, label} that producer tiles publish with one
+//     sc1 store each (the data is the flag: cdna_hip_programming.md G16 R2) plus a
+//     gather of the triangle's vertices from the read-only soup.  Readiness and
+//     ring capacity are LDS counters; the helper waits on global memory, the
+//     compute wave never does.
+// Tasks are dequeued in anti-diagonal order (J+K, then J) from an atomic counter,
+// so every producer tile is claimed by a running workgroup before its consumers:
+// no residency assumption and no deadlock.  Every spin is bounded (watchdog).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <vector>
+
+#include "geom.hpp"
+
+namespace sdfhip {
+
+constexpr int ST_T = 8;                       // tile edge (b and c)
+constexpr int ST_NCOL = ST_T * ST_T;          // 64 columns = one wave
+constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edge (8), corner
+constexpr int ST_RO = 8;                      // own ring slots (steps)
+constexpr int ST_G = 4;                       // helper batch (steps / entries)
+constexpr int ST_RH = 8;                      // halo ring slots per stream
+constexpr int ST_THREADS = 128;               // compute wave + helper wave
+constexpr int ST_RING0 = 0;                                   // 4 slots x 64 columns
+constexpr int ST_HALO0 = ST_RING0 + 4 * ST_NCOL;              // 17 streams x RH
+constexpr int ST_OWN0 = ST_HALO0 + ST_NSTREAM * ST_RH;        // RO slots x 64 columns
+constexpr int ST_ENTS = ST_OWN0 + ST_RO * ST_NCOL;
+constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
+
+struct StParams {
+    const float4 *soup;           // 3 float4 per triangle (xyz; w unused)
+    unsigned long long *cell;     // (phi bits << 32) | closest_tri, i-fastest
+    unsigned long long *hb;       // granules of tile-row edges:  [nJ][C][A]
+    unsigned long long *hc;       // granules of tile-column edges: [nK][B][A]
+    const int2 *tasks;            // (J,K) in dequeue order
+    int *queue;                   // task counter (zeroed before each launch)
+    int *err;                     // bit 1: watchdog fired
+    unsigned long long *stats;    // optional [evaluations, compute polls, helper polls]
+    float ox, oy, oz, dx;
+    int ni, nj, nk;
+    int A, B, C, nJ, nK, ntasks;
+    int di, dj, dk;
+    unsigned epoch;
+};
+
+__device__ __forceinline__ size_t st_phys(const StParams &P, int a, int b, int c)
+{
+    const int i = P.di > 0 ? a + 1 : P.ni - 2 - a;
+    const int j = P.dj > 0 ? b + 1 : P.nj - 2 - b;
+    const int k = P.dk > 0 ? c + 1 : P.nk - 2 - c;
+    return (size_t)i + (size_t)P.ni * ((size_t)j + (size_t)P.nj * (size_t)k);
+}
+
+__device__ __forceinline__ f3 st_gx(const StParams &P, int a, int b, int c)
+{
+    const int i = P.di > 0 ? a + 1 : P.ni - 2 - a;
+    const int j = P.dj > 0 ? b + 1 : P.nj - 2 - b;
+    const int k = P.dk > 0 ? c + 1 : P.nk - 2 - c;
+    return mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
+}
+
+__device__ __forceinline__ f3 st_xyz(float4 v) { return mk3(v.x, v.y, v.z); }
+
+__device__ __forceinline__ int lds_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// all of this wave's LDS writes have executed before anything after this point
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v0, float4 &v1, float4 &v2)
+{
+    if (t >= 0) {
+        v0 = soup[3 * (size_t)t];
+        v1 = soup[3 * (size_t)t + 1];
+        v2 = soup[3 * (size_t)t + 2];
+    } else {
+        v0 = v1 = v2 = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+__global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
+{
+    __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
+    __shared__ int s_pair[7 * ST_NCOL];     // compacted (entry << 9 | q << 6 | lane) evaluation list
+    __shared__ float s_d[7 * ST_NCOL];      // distance of candidate q for lane
+    __shared__ int s_own_fill;              // own entries ready for steps < s_own_fill
+    __shared__ int s_halo_ready[ST_NSTREAM];  // halo entries < s_halo_ready[s] in LDS
+    __shared__ int s_progress;              // compute steps completed
+    __shared__ int s_abort;
+    __shared__ int s_task;
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int L = tid & 63;
+    const int bl = L & (ST_T - 1), cl = L >> 3;
+    unsigned long long n_evals = 0, n_cpoll = 0, n_hpoll = 0;
+
+    for (;;) {
+        if (tid == 0) s_task = atomicAdd(P.queue, 1);
+        __syncthreads();
+        const int task = s_task;
+        if (task >= P.ntasks) break;
+        const int2 JK = P.tasks[task];
+        const int J = JK.x, K = JK.y;
+        const int b0 = J * ST_T, c0 = K * ST_T;
+        const int nsteps = P.A + 2 * (ST_T - 1);
+        const int b = b0 + bl, c = c0 + cl;
+        const bool col = b < P.B && c < P.C;
+
+        // ---------------- task setup (both waves), then one barrier ----------------
+        if (wave == 0) {
+            // a = -1 entry of the own column (boundary plane, constant) -> ring slot 3
+            float4 v0, v1, v2;
+            int t = -1;
+            if (col) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
+            st_load_tri(P.soup, t, v0, v1, v2);
+            v0.w = __int_as_float(t);
+            const int e = ST_RING0 + 3 * ST_NCOL + L;
+            s_ent[3 * e] = v0;
+            s_ent[3 * e + 1] = v1;
+            s_ent[3 * e + 2] = v2;
+            if (L == 0) {
+                s_own_fill = 0;
+                s_progress = 0;
+                s_abort = 0;
+            }
+        } else if (L < ST_NSTREAM) {
+            int hb_ = 0, hc_ = 0;
+            bool valid;
+            if (L < ST_T) { hb_ = b0 - 1; hc_ = c0 + L; valid = hc_ < P.C; }
+            else if (L < 2 * ST_T) { hb_ = b0 + (L - ST_T); hc_ = c0 - 1; valid = hb_ < P.B; }
+            else { hb_ = b0 - 1; hc_ = c0 - 1; valid = true; }
+            float4 v0, v1, v2;
+            int t = -1;
+            if (valid) t = (int)(uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
+            st_load_tri(P.soup, t, v0, v1, v2);
+            v0.w = __int_as_float(t);
+            const int e = ST_HALO0 + L * ST_RH + (ST_RH - 1);
+            s_ent[3 * e] = v0;
+            s_ent[3 * e + 1] = v1;
+            s_ent[3 * e + 2] = v2;
+            s_halo_ready[L] = valid ? 0 : P.A;
+        }
+        __syncthreads();
+
+        if (wave == 0) {
+            // ======================= compute wave =======================
+            int nb_base[7], nb_stride[7], nb_mask[7];
+            {
+                auto ring = [&](int q, int lbl, int lcl) {
+                    nb_base[q] = ST_RING0 + lcl * ST_T + lbl;
+                    nb_stride[q] = ST_NCOL;
+                    nb_mask[q] = 3;
+                };
+                auto halo = [&](int q, int s) {
+                    nb_base[q] = ST_HALO0 + s * ST_RH;
+                    nb_stride[q] = 1;
+                    nb_mask[q] = ST_RH - 1;
+                };
+                ring(0, bl, cl);                                              // (a-1, b,   c)
+                if (bl > 0) { ring(1, bl - 1, cl); ring(2, bl - 1, cl); }     // (.,   b-1, c)
+                else { halo(1, cl); halo(2, cl); }
+                if (cl > 0) { ring(3, bl, cl - 1); ring(4, bl, cl - 1); }     // (.,   b,   c-1)
+                else { halo(3, ST_T + bl); halo(4, ST_T + bl); }
+                if (bl > 0 && cl > 0) { ring(5, bl - 1, cl - 1); ring(6, bl - 1, cl - 1); }   // (., b-1, c-1)
+                else if (bl == 0 && cl == 0) { halo(5, 2 * ST_T); halo(6, 2 * ST_T); }
+                else if (bl == 0) { halo(5, cl - 1); halo(6, cl - 1); }
+                else { halo(5, ST_T + bl - 1); halo(6, ST_T + bl - 1); }
+            }
+            unsigned polls = 0;
+            for (int h = 0; h < nsteps; ++h) {
+                const int a = h - bl - cl;
+                const bool act = col && a >= 0 && a < P.A;
+                // ---- wait until the helper has landed everything this step reads ----
+                for (;;) {
+                    bool ok = lds_ld(&s_own_fill) > h;
+                    if (act) {
+                        if (bl == 0 && lds_ld(&s_halo_ready[cl]) <= a) ok = false;
+                        if (cl == 0 && lds_ld(&s_halo_ready[ST_T + bl]) <= a) ok = false;
+                        if (bl == 0 && cl == 0 && lds_ld(&s_halo_ready[2 * ST_T]) <= a) ok = false;
+                    }
+                    if (__all(ok)) break;
+                    ++n_cpoll;
+                    if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
+                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); }
+                        h = nsteps;
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
+                if (h >= nsteps) break;
+                polls = 0;
+                // ---- candidates: the 7 upwind labels minus exact duplicates ----
+                float phi = 0.f;
+                int ct = -1, ct_orig = -1, win = -1;
+                int lab[7], ent[7];
+                unsigned fmask = 0;
+                const int e_own = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + L;
+                if (act) {
+                    const float4 o0 = s_ent[3 * e_own], o1 = s_ent[3 * e_own + 1];
+                    ct = __float_as_int(o0.w);
+                    phi = o1.w;
+                    ct_orig = ct;
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        const int aq = (q & 1) == 0 ? a - 1 : a;   // q = 0,2,4,6 read a-1
+                        ent[q] = nb_base[q] + (aq & nb_mask[q]) * nb_stride[q];
+                        lab[q] = __float_as_int(s_ent[3 * ent[q]].w);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        bool skip = (lab[q] < 0) || (lab[q] == ct_orig);
+#pragma unroll
+                        for (int r = 0; r < q; ++r) skip = skip || (lab[r] == lab[q]);
+                        if (!skip) fmask |= 1u << q;
+                    }
+                }
+                // ---- compact (cell, candidate) pairs across the wave ----
+                int total = 0;
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    const bool f = (fmask >> q) & 1u;
+                    const unsigned long long m = __ballot(f);
+                    if (f) {
+                        const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        s_pair[pos] = (ent[q] << 9) | (q << 6) | L;
+                    }
+                    total += (int)__popcll(m);
+                }
+                // ---- evaluate two pairs per lane per round (independent chains) ----
+                for (int k = L; k < total; k += 128) {
+                    const int p1 = s_pair[k];
+                    const bool has2 = k + 64 < total;
+                    const int p2 = has2 ? s_pair[k + 64] : p1;
+                    const int l1 = p1 & 63, l2 = p2 & 63;
+                    const int e1 = p1 >> 9, e2 = p2 >> 9;
+                    const f3 g1 = st_gx(P, h - (l1 & 7) - (l1 >> 3), b0 + (l1 & 7), c0 + (l1 >> 3));
+                    const f3 g2 = st_gx(P, h - (l2 & 7) - (l2 >> 3), b0 + (l2 & 7), c0 + (l2 >> 3));
+                    const float d1 = ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
+                    const float d2 = ptd_nb(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
+                    s_d[((p1 >> 6) & 7) * ST_NCOL + l1] = d1;
+                    if (has2) s_d[((p2 >> 6) & 7) * ST_NCOL + l2] = d2;
+                }
+                n_evals += (L == 0) ? (unsigned long long)total : 0ull;
+                // ---- apply in the reference check order: strict '<', first minimum wins ----
+                if (act) {
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        if ((fmask >> q) & 1u) {
+                            const float d = s_d[q * ST_NCOL + L];
+                            if (d < phi) {
+                                phi = d;
+                                ct = lab[q];
+                                win = ent[q];
+                            }
+                        }
+                    }
+                    const int src = win < 0 ? e_own : win;
+                    float4 w0 = s_ent[3 * src];
+                    const float4 w1 = s_ent[3 * src + 1], w2 = s_ent[3 * src + 2];
+                    w0.w = __int_as_float(ct);
+                    const int slot = ST_RING0 + (a & 3) * ST_NCOL + L;
+                    s_ent[3 * slot] = w0;
+                    s_ent[3 * slot + 1] = w1;
+                    s_ent[3 * slot + 2] = w2;
+                    if (win >= 0)
+                        P.cell[st_phys(P, a, b, c)] = ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
+                    const unsigned long long gran = ((unsigned long long)P.epoch << 32) | (uint32_t)ct;
+                    if (bl == ST_T - 1 && J < P.nJ - 1)
+                        __hip_atomic_store(P.hb + ((size_t)J * P.C + c) * P.A + a, gran, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    if (cl == ST_T - 1 && K < P.nK - 1)
+                        __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
+                lds_drain();
+                if (L == 0) lds_st(&s_progress, h + 1);
+            }
+        } else {
+            // ======================= helper wave =======================
+            // stream geometry (lanes < 17)
+            const bool hlane = L < ST_NSTREAM;
+            int hbs = 0, hcs = 0, hoff = 0;
+            bool hvalid = false, hbound = true;
+            const unsigned long long *hsrc = nullptr;
+            if (hlane) {
+                if (L < ST_T) {
+                    hbs = b0 - 1; hcs = c0 + L; hoff = L; hvalid = hcs < P.C; hbound = (J == 0);
+                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
+                } else if (L < 2 * ST_T) {
+                    hbs = b0 + (L - ST_T); hcs = c0 - 1; hoff = L - ST_T; hvalid = hbs < P.B; hbound = (K == 0);
+                    if (!hbound) hsrc = P.hc + ((size_t)(K - 1) * P.B + hbs) * P.A;
+                } else {
+                    hbs = b0 - 1; hcs = c0 - 1; hoff = 0; hvalid = true; hbound = (J == 0 || K == 0);
+                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
+                }
+            }
+            int own_f = 0;                    // own entries filled for steps < own_f
+            int hnext = hvalid ? 0 : P.A;     // next halo entry to fill
+            unsigned idle = 0;
+            for (;;) {
+                const int prog = lds_ld(&s_progress);
+                if (lds_ld(&s_abort)) break;
+                asm volatile("" ::: "memory");   // ring writes below stay after the capacity read
+                // ---- own batch: steps [own_f, own_f + gcnt) ----
+                int gcnt = min(ST_G, min(nsteps - own_f, prog + ST_RO - own_f));
+                if (gcnt < 0) gcnt = 0;
+                unsigned long long cv[ST_G];
+#pragma unroll
+                for (int g = 0; g < ST_G; ++g) {
+                    const int a = own_f + g - bl - cl;
+                    cv[g] = 0xffffffffull;
+                    if (g < gcnt && col && a >= 0 && a < P.A) cv[g] = P.cell[st_phys(P, a, b, c)];
+                }
+                // ---- halo batch: entries [hnext, hnext + hcnt) ----
+                int hcnt = 0;
+                unsigned long long gv[ST_G];
+                if (hvalid) {
+                    hcnt = min(ST_G, min(P.A - hnext, prog + ST_RH - hoff - 2 - hnext));
+                    if (hcnt < 0) hcnt = 0;
+                }
+#pragma unroll
+                for (int g = 0; g < ST_G; ++g) {
+                    gv[g] = 0;
+                    if (g < hcnt) {
+                        if (hbound) gv[g] = P.cell[st_phys(P, hnext + g, hbs, hcs)];
+                        else gv[g] = __hip_atomic_load(hsrc + hnext + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                // ready prefix of the halo batch (tag == epoch; boundary planes always ready)
+                int hp = 0;
+#pragma unroll
+                for (int g = 0; g < ST_G; ++g)
+                    if (hp == g && g < hcnt && (hbound || (uint32_t)(gv[g] >> 32) == P.epoch)) hp = g + 1;
+                // ---- gather vertices ----
+                float4 ov[ST_G][3], hv[ST_G][3];
+#pragma unroll
+                for (int g = 0; g < ST_G; ++g) {
+                    st_load_tri(P.soup, (int)(uint32_t)cv[g], ov[g][0], ov[g][1], ov[g][2]);
+                    st_load_tri(P.soup, g < hp ? (int)(uint32_t)gv[g] : -1, hv[g][0], hv[g][1], hv[g][2]);
+                }
+                // ---- land in LDS, then publish readiness ----
+#pragma unroll
+                for (int g = 0; g < ST_G; ++g) {
+                    const int a = own_f + g - bl - cl;
+                    if (g < gcnt && col && a >= 0 && a < P.A) {
+                        const int e = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + L;
+                        float4 v0 = ov[g][0], v1 = ov[g][1];
+                        v0.w = __int_as_float((int)(uint32_t)cv[g]);
+                        v1.w = __uint_as_float((uint32_t)(cv[g] >> 32));
+                        s_ent[3 * e] = v0;
+                        s_ent[3 * e + 1] = v1;
+                        s_ent[3 * e + 2] = ov[g][2];
+                    }
+                    if (g < hp) {
+                        const int e = ST_HALO0 + L * ST_RH + ((hnext + g) & (ST_RH - 1));
+                        float4 v0 = hv[g][0];
+                        v0.w = __int_as_float((int)(uint32_t)gv[g]);
+                        s_ent[3 * e] = v0;
+                        s_ent[3 * e + 1] = hv[g][1];
+                        s_ent[3 * e + 2] = hv[g][2];
+                    }
+                }
+                lds_drain();
+                own_f += gcnt;
+                hnext += hp;
+                if (L == 0) lds_st(&s_own_fill, own_f);
+                if (hvalid && hp) lds_st(&s_halo_ready[L], hnext);
+                const bool done = own_f >= nsteps && hnext >= P.A;
+                if (__all(done)) break;
+                if (__any(gcnt > 0 || hp > 0)) {
+                    idle = 0;
+                } else {
+                    ++n_hpoll;
+                    if (++idle > ST_WATCHDOG) {
+                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); }
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (P.stats && L == 0) {
+        if (n_evals) atomicAdd(P.stats, n_evals);
+        if (n_cpoll) atomicAdd(P.stats + 1, n_cpoll);
+        if (n_hpoll) atomicAdd(P.stats + 2, n_hpoll);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct TileSweepWorkspace {
+    unsigned long long *hb = nullptr, *hc = nullptr, *stats = nullptr;
+    size_t cap_hb = 0, cap_hc = 0;
+    int2 *tasks = nullptr;
+    size_t cap_tasks = 0;
+    int task_nJ = -1, task_nK = -1;
+    int *ctrl = nullptr;   // [0] queue counter, [1] error bits
+    unsigned epoch = 0;
+    bool count = false;
+};
+
+inline bool tile_sweep_supported(int ni, int nj, int nk) { return ni >= 2 && nj >= 2 && nk >= 2; }
+
+inline int st_grow(unsigned long long **p, size_t *cap, size_t need)
+{
+    if (*p && *cap >= need) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void **)p, need * sizeof(unsigned long long)) != hipSuccess) return -5;
+    // tags are epochs >= 1: zeroed granules can never look published
+    if (hipMemset(*p, 0, need * sizeof(unsigned long long)) != hipSuccess) return -4;
+    *cap = need;
+    return 0;
+}
+
+// Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
+inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
+                      const float origin[3], float dx, int ni, int nj, int nk, int di, int dj, int dk, char *err,
+                      size_t errlen)
+{
+    const int A = ni - 1, B = nj - 1, C = nk - 1;
+    const int nJ = (B + ST_T - 1) / ST_T, nK = (C + ST_T - 1) / ST_T;
+    const int ntasks = nJ * nK;
+    auto fail = [&](int code, const char *msg) {
+        if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
+        return code;
+    };
+    if (st_grow(&W.hb, &W.cap_hb, (size_t)nJ * C * A)) return fail(-5, "halo buffer allocation failed");
+    if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A)) return fail(-5, "halo buffer allocation failed");
+    if (!W.ctrl) {
+        if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
+        if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
+        if (hipMemset(W.ctrl, 0, 16 * sizeof(int)) != hipSuccess) return fail(-4, "memset");
+    }
+    if (W.task_nJ != nJ || W.task_nK != nK) {
+        std::vector<int2> t;
+        t.reserve(ntasks);
+        for (int d = 0; d <= nJ + nK - 2; ++d)
+            for (int J = 0; J < nJ; ++J) {
+                const int K = d - J;
+                if (K >= 0 && K < nK) t.push_back(make_int2(J, K));
+            }
+        if ((size_t)ntasks > W.cap_tasks) {
+            if (W.tasks) (void)hipFree(W.tasks);
+            if (hipMalloc((void **)&W.tasks, ntasks * sizeof(int2)) != hipSuccess) return fail(-5, "task table");
+            W.cap_tasks = ntasks;
+        }
+        if (hipMemcpy(W.tasks, t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(-4, "task table upload");
+        W.task_nJ = nJ;
+        W.task_nK = nK;
+    }
+    if (++W.epoch == 0) ++W.epoch;
+    if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+    StParams P;
+    P.soup = soup;
+    P.cell = cell;
+    P.hb = W.hb;
+    P.hc = W.hc;
+    P.tasks = W.tasks;
+    P.queue = W.ctrl;
+    P.err = W.ctrl + 1;
+    P.stats = W.count ? W.stats : nullptr;
+    P.ox = origin[0];
+    P.oy = origin[1];
+    P.oz = origin[2];
+    P.dx = dx;
+    P.ni = ni;
+    P.nj = nj;
+    P.nk = nk;
+    P.A = A;
+    P.B = B;
+    P.C = C;
+    P.nJ = nJ;
+    P.nK = nK;
+    P.ntasks = ntasks;
+    P.di = di;
+    P.dj = dj;
+    P.dk = dk;
+    P.epoch = W.epoch;
+    const int grid = ntasks < 2048 ? ntasks : 2048;
+    hipLaunchKernelGGL(k_sweep_tile, dim3(grid), dim3(ST_THREADS), 0, st, P);
+    if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
+    return 0;
+}
+
+inline void tile_sweep_release(TileSweepWorkspace &W)
+{
+    (void)hipFree(W.hb);
+    (void)hipFree(W.hc);
+    (void)hipFree(W.tasks);
+    (void)hipFree(W.ctrl);
+    (void)hipFree(W.stats);
+    W = TileSweepWorkspace();
+}
+
+}  // namespace sdfhip

@@ -43,9 +43,10 @@ def _ptd_inputs(n, seed):
     return pts
 
 
-def test_device_ptd_bitwise_vs_oracle():
+@pytest.mark.parametrize("variant", [0, 1])
+def test_device_ptd_bitwise_vs_oracle(variant):
     pts = _ptd_inputs(4_000_000, 7)
-    got = _lib.debug_ptd(pts)
+    got = _lib.debug_ptd(pts, variant=variant)
     want = O.ptd_batch(pts)
     same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
     assert same.all(), f"{(~same).sum()} of {len(pts)} point-triangle distances differ"
@@ -169,6 +170,15 @@ def sweep_impl(request, monkeypatch):
     else:
         monkeypatch.delenv("SDFGEN_SWEEP", raising=False)
     return request.param
+
+
+@pytest.mark.parametrize("dims", [(2, 2, 2), (3, 2, 9), (9, 2, 3), (2, 17, 3), (10, 9, 17), (33, 8, 16), (5, 41, 9)])
+def test_gpu_sweep_impls_small_and_ragged_grids(sweep_impl, dims):
+    v, t = meshgen.bumpy_sphere(30, 13)
+    o, dx = meshgen.grid_mode2b(v, max(dims[0], 5), max(dims[1], 5), max(dims[2], 5), 1)
+    want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, *dims, exact_band=1))
+    got = _lib.make_level_set3(v, t, o, dx, *dims, 1)
+    assert bits_equal(got, want), diff_report(got, want, dx)
 
 
 @pytest.mark.parametrize("nu,nv,dims", [(90, 31, (57, 33, 70)), (40, 21, (17, 40, 35)), (200, 61, (64, 48, 40))])
