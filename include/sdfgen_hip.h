@@ -100,6 +100,7 @@ typedef struct sdfgen_hip_profile {
     uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless SDFGEN_COUNT_EVALS is set) */
     uint64_t sweep_stalls;    /* compute-wave polls that found a hand-off not yet landed (same) */
     uint64_t helper_polls;    /* helper-wave polls that found nothing to fetch (same) */
+    uint64_t own_waits;       /* compute-wave polls waiting on the column prefetch (same) */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

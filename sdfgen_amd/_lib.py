@@ -50,6 +50,7 @@ class Profile(ctypes.Structure):
         ("sweep_evals", ctypes.c_uint64),
         ("sweep_stalls", ctypes.c_uint64),
         ("helper_polls", ctypes.c_uint64),
+        ("own_waits", ctypes.c_uint64),
     ]
 
     def as_dict(self):

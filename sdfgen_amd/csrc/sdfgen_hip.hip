@@ -483,6 +483,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sweep_evals = wf_stats[0];
     p.sweep_stalls = wf_stats[1];
     p.helper_polls = wf_stats[2];
+    p.own_waits = wf_stats[3];
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;

@@ -64,7 +64,7 @@ struct StParams {
     const int2 *tasks;            // (J,K) in dequeue order
     int *queue;                   // task counter (zeroed before each launch)
     int *err;                     // bit 1: watchdog fired
-    unsigned long long *stats;    // optional [evaluations, compute polls, helper polls]
+    unsigned long long *stats;    // optional [evaluations, compute polls, helper idle polls, compute polls on own data]
     float ox, oy, oz, dx;
     int ni, nj, nk;
     int A, B, C, nJ, nK, ntasks;
@@ -121,7 +121,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
     const int wave = tid >> 6;
     const int L = tid & 63;
     const int bl = L & (ST_T - 1), cl = L >> 3;
-    unsigned long long n_evals = 0, n_cpoll = 0, n_hpoll = 0;
+    unsigned long long n_evals = 0, n_cpoll = 0, n_hpoll = 0, n_cpoll_own = 0;
 
     for (;;) {
         if (tid == 0) s_task = atomicAdd(P.queue, 1);
@@ -142,9 +142,8 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             int t = -1;
             if (col) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
             st_load_tri(P.soup, t, v0, v1, v2);
-            v0.w = __int_as_float(t);
             const int e = ST_RING0 + 3 * ST_NCOL + L;
-            s_ent[3 * e] = v0;
+            s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
             s_ent[3 * e + 1] = v1;
             s_ent[3 * e + 2] = v2;
             if (L == 0) {
@@ -162,9 +161,8 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             int t = -1;
             if (valid) t = (int)(uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
             st_load_tri(P.soup, t, v0, v1, v2);
-            v0.w = __int_as_float(t);
             const int e = ST_HALO0 + L * ST_RH + (ST_RH - 1);
-            s_ent[3 * e] = v0;
+            s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
             s_ent[3 * e + 1] = v1;
             s_ent[3 * e + 2] = v2;
             s_halo_ready[L] = valid ? 0 : P.A;
@@ -201,7 +199,8 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 const bool act = col && a >= 0 && a < P.A;
                 // ---- wait until the helper has landed everything this step reads ----
                 for (;;) {
-                    bool ok = lds_ld(&s_own_fill) > h;
+                    const bool own_ok = lds_ld(&s_own_fill) > h;
+                    bool ok = own_ok;
                     if (act) {
                         if (bl == 0 && lds_ld(&s_halo_ready[cl]) <= a) ok = false;
                         if (cl == 0 && lds_ld(&s_halo_ready[ST_T + bl]) <= a) ok = false;
@@ -209,6 +208,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     }
                     if (__all(ok)) break;
                     ++n_cpoll;
+                    if (!__all(own_ok)) ++n_cpoll_own;
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
                         if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); }
                         h = nsteps;
@@ -286,11 +286,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                         }
                     }
                     const int src = win < 0 ? e_own : win;
-                    float4 w0 = s_ent[3 * src];
+                    const float4 w0 = s_ent[3 * src];
                     const float4 w1 = s_ent[3 * src + 1], w2 = s_ent[3 * src + 2];
-                    w0.w = __int_as_float(ct);
                     const int slot = ST_RING0 + (a & 3) * ST_NCOL + L;
-                    s_ent[3 * slot] = w0;
+                    s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __int_as_float(ct));
                     s_ent[3 * slot + 1] = w1;
                     s_ent[3 * slot + 2] = w2;
                     if (win >= 0)
@@ -325,80 +324,100 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
                 }
             }
-            int own_f = 0;                    // own entries filled for steps < own_f
-            int hnext = hvalid ? 0 : P.A;     // next halo entry to fill
+            if (!hvalid || hbound) hsrc = P.hb;   // any valid address: unused lanes load harmlessly
+            // Two-stage software pipeline, one global round trip per iteration:
+            //   stage 1 (batch B): the columns' old cells and the halo granules;
+            //   stage 2 (batch A, loaded last iteration): gather the labels' vertices,
+            //   land them in LDS and publish readiness.
+            // All loads are unconditional (invalid slots read a clamped address and are
+            // ignored), so hipcc's waitcnt pass can count them and waits for the stage-2
+            // gathers only, leaving the younger stage-1 loads in flight.
+            int fA = 0, gA = 0;                    // own steps [fA, fA+gA) whose cells are in c0..c3
+            int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
+            unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
+            unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
+            static_assert(ST_G == 4, "helper pipeline is written out for 4-element batches");
             unsigned idle = 0;
             for (;;) {
                 const int prog = lds_ld(&s_progress);
                 if (lds_ld(&s_abort)) break;
-                asm volatile("" ::: "memory");   // ring writes below stay after the capacity read
-                // ---- own batch: steps [own_f, own_f + gcnt) ----
-                int gcnt = min(ST_G, min(nsteps - own_f, prog + ST_RO - own_f));
-                if (gcnt < 0) gcnt = 0;
-                unsigned long long cv[ST_G];
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
-                    const int a = own_f + g - bl - cl;
-                    cv[g] = 0xffffffffull;
-                    if (g < gcnt && col && a >= 0 && a < P.A) cv[g] = P.cell[st_phys(P, a, b, c)];
-                }
-                // ---- halo batch: entries [hnext, hnext + hcnt) ----
-                int hcnt = 0;
-                unsigned long long gv[ST_G];
+                // The batch-A loads were issued one iteration ago: wait for them once, and hand
+                // the registers back through the asm so the compiler does not track them as
+                // pending (its per-use waits would otherwise serialise the gathers below).
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(q0), "+v"(q1),
+                             "+v"(q2), "+v"(q3)::"memory");
+                // ---- stage 2: vertices for batch A ----
+                int hp = 0;   // ready prefix of the halo batch (tag == epoch; boundary planes always)
+                const bool r0 = hbound || (uint32_t)(q0 >> 32) == P.epoch;
+                const bool r1 = hbound || (uint32_t)(q1 >> 32) == P.epoch;
+                const bool r2 = hbound || (uint32_t)(q2 >> 32) == P.epoch;
+                const bool r3 = hbound || (uint32_t)(q3 >> 32) == P.epoch;
+                if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
+#define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
+#define ST_GATHER(g, cg, qg)                                                                          \
+    const size_t so##g = 3 * (size_t)(ST_OWN_OK(g) && (int)(uint32_t)(cg) >= 0 ? (uint32_t)(cg) : 0u); \
+    const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
+    const size_t sh##g = 3 * (size_t)((g) < hp && (int)(uint32_t)(qg) >= 0 ? (uint32_t)(qg) : 0u);     \
+    const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
+                ST_GATHER(0, c0, q0)
+                ST_GATHER(1, c1, q1)
+                ST_GATHER(2, c2, q2)
+                ST_GATHER(3, c3, q3)
+                // ---- stage 1: issue batch B ----
+                const int fB = fA + gA;
+                int gB = min(ST_G, min(nsteps - fB, prog + ST_RO - fB));
+                if (gB < 0) gB = 0;
+                const int hB = hA + hp;
+                int hcB = 0;
                 if (hvalid) {
-                    hcnt = min(ST_G, min(P.A - hnext, prog + ST_RH - hoff - 2 - hnext));
-                    if (hcnt < 0) hcnt = 0;
+                    hcB = min(ST_G, min(P.A - hB, prog + ST_RH - hoff - 2 - hB));
+                    if (hcB < 0) hcB = 0;
                 }
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
-                    gv[g] = 0;
-                    if (g < hcnt) {
-                        if (hbound) gv[g] = P.cell[st_phys(P, hnext + g, hbs, hcs)];
-                        else gv[g] = __hip_atomic_load(hsrc + hnext + g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-                // ready prefix of the halo batch (tag == epoch; boundary planes always ready)
-                int hp = 0;
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g)
-                    if (hp == g && g < hcnt && (hbound || (uint32_t)(gv[g] >> 32) == P.epoch)) hp = g + 1;
-                // ---- gather vertices ----
-                float4 ov[ST_G][3], hv[ST_G][3];
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
-                    st_load_tri(P.soup, (int)(uint32_t)cv[g], ov[g][0], ov[g][1], ov[g][2]);
-                    st_load_tri(P.soup, g < hp ? (int)(uint32_t)gv[g] : -1, hv[g][0], hv[g][1], hv[g][2]);
-                }
-                // ---- land in LDS, then publish readiness ----
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
-                    const int a = own_f + g - bl - cl;
-                    if (g < gcnt && col && a >= 0 && a < P.A) {
-                        const int e = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + L;
-                        float4 v0 = ov[g][0], v1 = ov[g][1];
-                        v0.w = __int_as_float((int)(uint32_t)cv[g]);
-                        v1.w = __uint_as_float((uint32_t)(cv[g] >> 32));
-                        s_ent[3 * e] = v0;
-                        s_ent[3 * e + 1] = v1;
-                        s_ent[3 * e + 2] = ov[g][2];
-                    }
-                    if (g < hp) {
-                        const int e = ST_HALO0 + L * ST_RH + ((hnext + g) & (ST_RH - 1));
-                        float4 v0 = hv[g][0];
-                        v0.w = __int_as_float((int)(uint32_t)gv[g]);
-                        s_ent[3 * e] = v0;
-                        s_ent[3 * e + 1] = hv[g][1];
-                        s_ent[3 * e + 2] = hv[g][2];
-                    }
-                }
+#define ST_ISSUE(g, cn, qn)                                                                            \
+    unsigned long long cn, qn;                                                                         \
+    {                                                                                                  \
+        const int a_ = fB + (g) - bl - cl;                                                             \
+        const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
+        cn = P.cell[ok_ ? st_phys(P, a_, b, c) : 0];                                                   \
+        const unsigned long long *src_ =                                                               \
+            (g) >= hcB ? P.hb : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g));  \
+        qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                      \
+    }
+                ST_ISSUE(0, n0, m0)
+                ST_ISSUE(1, n1, m1)
+                ST_ISSUE(2, n2, m2)
+                ST_ISSUE(3, n3, m3)
+                // ---- land batch A in LDS, then publish readiness ----
+#define ST_LAND(g, cg, qg)                                                                             \
+    if (ST_OWN_OK(g)) {                                                                                \
+        const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + L;                   \
+        s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __int_as_float((int)(uint32_t)(cg)));   \
+        s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
+        s_ent[3 * e_ + 2] = oc##g;                                                                     \
+    }                                                                                                  \
+    if ((g) < hp) {                                                                                    \
+        const int e_ = ST_HALO0 + L * ST_RH + ((hA + (g)) & (ST_RH - 1));                              \
+        s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __int_as_float((int)(uint32_t)(qg)));   \
+        s_ent[3 * e_ + 1] = hb##g;                                                                     \
+        s_ent[3 * e_ + 2] = hc##g;                                                                     \
+    }
+                ST_LAND(0, c0, q0)
+                ST_LAND(1, c1, q1)
+                ST_LAND(2, c2, q2)
+                ST_LAND(3, c3, q3)
+#undef ST_OWN_OK
+#undef ST_GATHER
+#undef ST_ISSUE
+#undef ST_LAND
                 lds_drain();
-                own_f += gcnt;
-                hnext += hp;
-                if (L == 0) lds_st(&s_own_fill, own_f);
-                if (hvalid && hp) lds_st(&s_halo_ready[L], hnext);
-                const bool done = own_f >= nsteps && hnext >= P.A;
-                if (__all(done)) break;
-                if (__any(gcnt > 0 || hp > 0)) {
+                if (L == 0 && gA) lds_st(&s_own_fill, fB);
+                if (hvalid && hp) lds_st(&s_halo_ready[L], hB);
+                const bool moved = gA > 0 || hp > 0 || gB > 0 || hcB > 0;
+                fA = fB; gA = gB; hA = hB; hcA = hcB;
+                c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+                q0 = m0; q1 = m1; q2 = m2; q3 = m3;
+                if (__all(fB >= nsteps && gB == 0 && hB >= P.A)) break;
+                if (__any(moved)) {
                     idle = 0;
                 } else {
                     ++n_hpoll;
@@ -416,6 +435,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
         if (n_evals) atomicAdd(P.stats, n_evals);
         if (n_cpoll) atomicAdd(P.stats + 1, n_cpoll);
         if (n_hpoll) atomicAdd(P.stats + 2, n_hpoll);
+        if (n_cpoll_own) atomicAdd(P.stats + 3, n_cpoll_own);
     }
 }
 

@@ -144,20 +144,43 @@ def test_gpu_bad_index_raises():
         _lib.make_level_set3(v, t, (0, 0, 0), 0.1, 8, 8, 8, 1)
 
 
-def test_gpu_device_entry_with_torch_buffers():
-    torch = pytest.importorskip("torch")
+def _hip_runtime():
+    """The HIP runtime libsdfgen_hip.so itself links (same process-wide instance)."""
+    import ctypes
+    rt = ctypes.CDLL("libamdhip64.so.7")
+    rt.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    rt.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    rt.hipFree.argtypes = [ctypes.c_void_p]
+    return rt
+
+
+def test_gpu_device_entry_with_device_buffers():
+    """sdfgen_hip_make_level_set3_device on caller-owned HBM buffers (no torch: torch
+    bundles its own HIP runtime)."""
+    import ctypes
+    rt = _hip_runtime()
     v, t = meshgen.bumpy_sphere(100, 41)
     o, dx = meshgen.grid_mode2b(v, 40, 36, 44, 2)
-    dev = torch.device("cuda:0")
-    dv = torch.from_numpy(v).to(dev)
-    dt = torch.from_numpy(t.view(np.int32)).to(dev)
-    out = torch.empty(40 * 36 * 44, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    _lib.make_level_set3_device(0, dt.data_ptr(), t.shape[0], dv.data_ptr(), v.shape[0], o, dx, 40, 36, 44, 1,
-                                _lib.LAYOUT_KFAST, out.data_ptr(), stream.cuda_stream)
-    got = out.cpu().numpy().reshape(40, 36, 44)
+    n = 40 * 36 * 44
+    bufs = []
+    def dmalloc(nbytes):
+        p = ctypes.c_void_p()
+        assert rt.hipMalloc(ctypes.byref(p), nbytes) == 0
+        bufs.append(p)
+        return p.value
+    try:
+        dv, dt, dout = dmalloc(v.nbytes), dmalloc(t.nbytes), dmalloc(4 * n)
+        assert rt.hipMemcpy(dv, v.ctypes.data, v.nbytes, 1) == 0
+        assert rt.hipMemcpy(dt, t.ctypes.data, t.nbytes, 1) == 0
+        _lib.make_level_set3_device(0, dt, t.shape[0], dv, v.shape[0], o, dx, 40, 36, 44, 1,
+                                    _lib.LAYOUT_KFAST, dout)
+        got = np.empty(n, np.float32)
+        assert rt.hipMemcpy(got.ctypes.data, dout, 4 * n, 2) == 0
+    finally:
+        for p in bufs:
+            rt.hipFree(p)
     want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, 40, 36, 44, 1))
-    assert bits_equal(got, want), diff_report(got, want, dx)
+    assert bits_equal(got.reshape(40, 36, 44), want), diff_report(got.reshape(40, 36, 44), want, dx)
     prof = _lib.last_profile()
     assert prof["total_ms"] > 0 and prof["band_evals"] > 0
 

@@ -22,7 +22,8 @@ for mode in ("timing", "count"):
         p = _lib.last_profile()
         print(f"{mode} rep{r}: wall {el*1e3:.1f} ms  total {p['total_ms']:.2f}  band {p['band_ms']:.2f}  "
               f"sweep {p['sweep_ms']:.2f}  sign {p['sign_ms']:.3f}  impl {p['sweep_impl']}  "
-              f"band_evals {p['band_evals']}  sweep_evals {p['sweep_evals']}  stalls {p['sweep_stalls']}",
+              f"band_evals {p['band_evals']}  sweep_evals {p['sweep_evals']}  stalls {p['sweep_stalls']} "
+              f"(own {p['own_waits']})  helper_idle {p['helper_polls']}",
               flush=True)
     print("per-sweep ms:", [round(x, 3) for x in p["sweep_launch_ms"]], flush=True)
 ncell = np.prod(dims)
