@@ -33,6 +33,7 @@ EXPORTED = (
     "sdfgen_hip_debug_ptd",
     "sdfgen_hip_debug_pit2d",
     "sdfgen_cpu_make_level_set3",
+    "sdfgen_hip_debug_sweep_trace",
 )
 
 
@@ -86,6 +87,8 @@ def _load():
     L.sdfgen_hip_debug_ptd.restype = ctypes.c_int
     L.sdfgen_hip_debug_pit2d.argtypes = [ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
     L.sdfgen_hip_debug_pit2d.restype = ctypes.c_int
+    L.sdfgen_hip_debug_sweep_trace.argtypes = [ctypes.c_int, _P, _u64, ctypes.POINTER(_u64)]
+    L.sdfgen_hip_debug_sweep_trace.restype = ctypes.c_int
     return L
 
 
@@ -187,6 +190,15 @@ def debug_ptd(pts: np.ndarray, device: int = 0, variant: int = 0) -> np.ndarray:
     if rc != OK:
         _raise(rc, err)
     return out
+
+
+def debug_sweep_trace(device: int = 0, max_entries: int = 1 << 22) -> np.ndarray:
+    out = np.zeros(max_entries, np.uint64)
+    n = _u64(0)
+    rc = lib.sdfgen_hip_debug_sweep_trace(device, out.ctypes.data_as(_P), max_entries, ctypes.byref(n))
+    if rc != OK:
+        raise RuntimeError("no sweep trace recorded (set SDFGEN_TRACE_SWEEP)")
+    return out[: n.value].reshape(-1, 2)
 
 
 def debug_pit2d(pit: np.ndarray, device: int = 0) -> np.ndarray:

@@ -416,6 +416,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         const char *e = getenv("SDFGEN_SWEEP");  // diagnostics: "plane" forces the hyperplane launches
         if (e && strcmp(e, "plane") == 0) impl = 0;
         ws->wf.count = getenv("SDFGEN_COUNT_EVALS") != nullptr;
+        const char *tr = getenv("SDFGEN_TRACE_SWEEP");   // diagnostics: per-task timing of one sweep
+        ws->wf.trace_sweep = tr ? atoi(tr) : -1;
         if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 32, st));
     }
     for (int s = 0; s < 16; ++s) {
@@ -423,6 +425,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         if (!do_sweep) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
         if (impl == 1) {
+            ws->wf.cur_sweep = s;
             if ((rc = tile_sweep(ws->wf, st, ws->soup, ws->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
                                       err.len)))
                 return rc;
@@ -598,6 +601,25 @@ int sdfgen_hip_release(void)
         delete w;
     }
     g_ws.clear();
+    return 0;
+}
+
+int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries, uint64_t *n_out)
+{
+    Err err{nullptr, 0};
+    *n_out = 0;
+    Workspace *ws = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        for (Workspace *w : g_ws)
+            if (w->device == device) ws = w;
+    }
+    if (!ws || !ws->wf.trace) return SDFGEN_HIP_EINVAL;
+    std::lock_guard<std::mutex> lk(ws->mu);
+    HIPCHK(hipSetDevice(device));
+    const uint64_t n = std::min<uint64_t>(max_entries, ws->wf.cap_trace);
+    HIPCHK(hipMemcpy(out, ws->wf.trace, n * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    *n_out = n;
     return 0;
 }
 

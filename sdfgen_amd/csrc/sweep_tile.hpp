@@ -65,6 +65,7 @@ struct StParams {
     int *queue;                   // task counter (zeroed before each launch)
     int *err;                     // bit 1: watchdog fired
     unsigned long long *stats;    // optional [evaluations, compute polls, helper idle polls, compute polls on own data]
+    unsigned long long *trace;    // optional [task][start, end] wall_clock64 (100 MHz) of the compute wave
     float ox, oy, oz, dx;
     int ni, nj, nk;
     int A, B, C, nJ, nK, ntasks;
@@ -169,6 +170,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
         }
         __syncthreads();
 
+        if (P.trace && tid == 0) P.trace[2 * task] = wall_clock64();
         if (wave == 0) {
             // ======================= compute wave =======================
             int nb_base[7], nb_stride[7], nb_mask[7];
@@ -305,6 +307,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 lds_drain();
                 if (L == 0) lds_st(&s_progress, h + 1);
             }
+            if (P.trace && L == 0) P.trace[2 * task + 1] = wall_clock64();
         } else {
             // ======================= helper wave =======================
             // stream geometry (lanes < 17)
@@ -337,6 +340,8 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
             unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
             static_assert(ST_G == 4, "helper pipeline is written out for 4-element batches");
+            // unused load slots read this lane's own column start (spread, cached), never one hot address
+            const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, 0, 0);
             unsigned idle = 0;
             for (;;) {
                 const int prog = lds_ld(&s_progress);
@@ -374,19 +379,21 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     if (hcB < 0) hcB = 0;
                 }
 #define ST_ISSUE(g, cn, qn)                                                                            \
-    unsigned long long cn, qn;                                                                         \
     {                                                                                                  \
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
-        cn = P.cell[ok_ ? st_phys(P, a_, b, c) : 0];                                                   \
+        cn = P.cell[ok_ ? st_phys(P, a_, b, c) : dummy];                                               \
         const unsigned long long *src_ =                                                               \
-            (g) >= hcB ? P.hb : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g));  \
+            (g) >= hcB ? P.cell + dummy : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g)); \
         qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                      \
     }
-                ST_ISSUE(0, n0, m0)
-                ST_ISSUE(1, n1, m1)
-                ST_ISSUE(2, n2, m2)
-                ST_ISSUE(3, n3, m3)
+                unsigned long long n0 = ~0ull, n1 = ~0ull, n2 = ~0ull, n3 = ~0ull, m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+                if (__any(gB > 0 || hcB > 0)) {   // wave-uniform: idle helpers issue nothing
+                    ST_ISSUE(0, n0, m0)
+                    ST_ISSUE(1, n1, m1)
+                    ST_ISSUE(2, n2, m2)
+                    ST_ISSUE(3, n3, m3)
+                }
                 // ---- land batch A in LDS, then publish readiness ----
 #define ST_LAND(g, cg, qg)                                                                             \
     if (ST_OWN_OK(g)) {                                                                                \
@@ -443,7 +450,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
 // host side
 // ---------------------------------------------------------------------------
 struct TileSweepWorkspace {
-    unsigned long long *hb = nullptr, *hc = nullptr, *stats = nullptr;
+    unsigned long long *hb = nullptr, *hc = nullptr, *stats = nullptr, *trace = nullptr;
+    size_t cap_trace = 0;
+    int trace_sweep = -1;      // which sweep (0..15) to trace, -1 = none
+    int cur_sweep = 0;
     size_t cap_hb = 0, cap_hc = 0;
     int2 *tasks = nullptr;
     size_t cap_tasks = 0;
@@ -516,6 +526,11 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.queue = W.ctrl;
     P.err = W.ctrl + 1;
     P.stats = W.count ? W.stats : nullptr;
+    P.trace = nullptr;
+    if (W.trace_sweep >= 0 && W.trace_sweep == W.cur_sweep) {
+        if (st_grow(&W.trace, &W.cap_trace, 2 * (size_t)ntasks)) return fail(-5, "trace");
+        P.trace = W.trace;
+    }
     P.ox = origin[0];
     P.oy = origin[1];
     P.oz = origin[2];
@@ -546,6 +561,7 @@ inline void tile_sweep_release(TileSweepWorkspace &W)
     (void)hipFree(W.tasks);
     (void)hipFree(W.ctrl);
     (void)hipFree(W.stats);
+    (void)hipFree(W.trace);
     W = TileSweepWorkspace();
 }
 
