@@ -259,19 +259,29 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     }
                     total += (int)__popcll(m);
                 }
-                // ---- evaluate two pairs per lane per round (independent chains) ----
-                for (int k = L; k < total; k += 128) {
-                    const int p1 = s_pair[k];
-                    const bool has2 = k + 64 < total;
-                    const int p2 = has2 ? s_pair[k + 64] : p1;
-                    const int l1 = p1 & 63, l2 = p2 & 63;
-                    const int e1 = p1 >> 9, e2 = p2 >> 9;
-                    const f3 g1 = st_gx(P, h - (l1 & 7) - (l1 >> 3), b0 + (l1 & 7), c0 + (l1 >> 3));
-                    const f3 g2 = st_gx(P, h - (l2 & 7) - (l2 >> 3), b0 + (l2 & 7), c0 + (l2 >> 3));
-                    const float d1 = ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
-                    const float d2 = ptd_nb(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
-                    s_d[((p1 >> 6) & 7) * ST_NCOL + l1] = d1;
-                    if (has2) s_d[((p2 >> 6) & 7) * ST_NCOL + l2] = d2;
+                // ---- evaluate: one pair per lane, or two independent chains per lane ----
+                if (total <= ST_NCOL) {
+                    if (L < total) {
+                        const int p1 = s_pair[L];
+                        const int l1 = p1 & 63, e1 = p1 >> 9;
+                        const f3 g1 = st_gx(P, h - (l1 & 7) - (l1 >> 3), b0 + (l1 & 7), c0 + (l1 >> 3));
+                        s_d[((p1 >> 6) & 7) * ST_NCOL + l1] =
+                            ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
+                    }
+                } else {
+                    for (int k = L; k < total; k += 128) {
+                        const int p1 = s_pair[k];
+                        const bool has2 = k + 64 < total;
+                        const int p2 = has2 ? s_pair[k + 64] : p1;
+                        const int l1 = p1 & 63, l2 = p2 & 63;
+                        const int e1 = p1 >> 9, e2 = p2 >> 9;
+                        const f3 g1 = st_gx(P, h - (l1 & 7) - (l1 >> 3), b0 + (l1 & 7), c0 + (l1 >> 3));
+                        const f3 g2 = st_gx(P, h - (l2 & 7) - (l2 >> 3), b0 + (l2 & 7), c0 + (l2 >> 3));
+                        const float d1 = ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
+                        const float d2 = ptd_nb(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
+                        s_d[((p1 >> 6) & 7) * ST_NCOL + l1] = d1;
+                        if (has2) s_d[((p2 >> 6) & 7) * ST_NCOL + l2] = d2;
+                    }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
                 // ---- apply in the reference check order: strict '<', first minimum wins ----
@@ -419,7 +429,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 lds_drain();
                 if (L == 0 && gA) lds_st(&s_own_fill, fB);
                 if (hvalid && hp) lds_st(&s_halo_ready[L], hB);
-                const bool moved = gA > 0 || hp > 0 || gB > 0 || hcB > 0;
+                const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
                 fA = fB; gA = gB; hA = hB; hcA = hcB;
                 c0 = n0; c1 = n1; c2 = n2; c3 = n3;
                 q0 = m0; q1 = m1; q2 = m2; q3 = m3;
@@ -427,12 +437,16 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 if (__any(moved)) {
                     idle = 0;
                 } else {
+                    // back off (64..1024 cycles): hundreds of waiting tiles must not flood the
+                    // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
                     ++n_hpoll;
                     if (++idle > ST_WATCHDOG) {
                         if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); }
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(2);
+                    if (idle < 4) __builtin_amdgcn_s_sleep(1);
+                    else if (idle < 16) __builtin_amdgcn_s_sleep(4);
+                    else __builtin_amdgcn_s_sleep(16);
                 }
             }
         }
