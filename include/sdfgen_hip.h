@@ -118,7 +118,7 @@ int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, 
 int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *out4,
                            char *errbuf, size_t errlen);
 
-/* Diagnostics: per-task [start, end] wall-clock stamps (100 MHz) of the sweep named by
+/* Diagnostics: per-task [start, first step, middle step, end] wall-clock stamps (100 MHz) of the sweep named by
  * the SDFGEN_TRACE_SWEEP environment variable in the last call (tasks in dequeue order). */
 int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries, uint64_t *n_out);
 

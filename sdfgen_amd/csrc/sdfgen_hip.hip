@@ -418,6 +418,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->wf.count = getenv("SDFGEN_COUNT_EVALS") != nullptr;
         const char *tr = getenv("SDFGEN_TRACE_SWEEP");   // diagnostics: per-task timing of one sweep
         ws->wf.trace_sweep = tr ? atoi(tr) : -1;
+        const char *gr = getenv("SDFGEN_TILE_GRID");     // diagnostics: cap on resident workgroups
+        ws->wf.grid_override = gr ? atoi(gr) : 0;
         if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 32, st));
     }
     for (int s = 0; s < 16; ++s) {

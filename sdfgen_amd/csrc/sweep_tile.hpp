@@ -48,7 +48,7 @@ constexpr int ST_NCOL = ST_T * ST_T;          // 64 columns = one wave
 constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edge (8), corner
 constexpr int ST_RO = 8;                      // own ring slots (steps)
 constexpr int ST_G = 4;                       // helper batch (steps / entries)
-constexpr int ST_RH = 8;                      // halo ring slots per stream
+constexpr int ST_RH = 32;                     // halo ring slots per stream (lead = RH-3 steps)
 constexpr int ST_THREADS = 128;               // compute wave + helper wave
 constexpr int ST_RING0 = 0;                                   // 4 slots x 64 columns
 constexpr int ST_HALO0 = ST_RING0 + 4 * ST_NCOL;              // 17 streams x RH
@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
         }
         __syncthreads();
 
-        if (P.trace && tid == 0) P.trace[2 * task] = wall_clock64();
+        if (P.trace && tid == 0) P.trace[4 * task] = wall_clock64();
         if (wave == 0) {
             // ======================= compute wave =======================
             int nb_base[7], nb_stride[7], nb_mask[7];
@@ -316,8 +316,9 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 }
                 lds_drain();
                 if (L == 0) lds_st(&s_progress, h + 1);
+                if (P.trace && L == 0 && (h == 0 || h == nsteps / 2)) P.trace[4 * task + (h == 0 ? 1 : 2)] = wall_clock64();
             }
-            if (P.trace && L == 0) P.trace[2 * task + 1] = wall_clock64();
+            if (P.trace && L == 0) P.trace[4 * task + 3] = wall_clock64();
         } else {
             // ======================= helper wave =======================
             // stream geometry (lanes < 17)
@@ -468,6 +469,7 @@ struct TileSweepWorkspace {
     size_t cap_trace = 0;
     int trace_sweep = -1;      // which sweep (0..15) to trace, -1 = none
     int cur_sweep = 0;
+    int grid_override = 0;     // diagnostics: cap on resident workgroups
     size_t cap_hb = 0, cap_hc = 0;
     int2 *tasks = nullptr;
     size_t cap_tasks = 0;
@@ -542,7 +544,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.stats = W.count ? W.stats : nullptr;
     P.trace = nullptr;
     if (W.trace_sweep >= 0 && W.trace_sweep == W.cur_sweep) {
-        if (st_grow(&W.trace, &W.cap_trace, 2 * (size_t)ntasks)) return fail(-5, "trace");
+        if (st_grow(&W.trace, &W.cap_trace, 4 * (size_t)ntasks)) return fail(-5, "trace");
         P.trace = W.trace;
     }
     P.ox = origin[0];
@@ -562,7 +564,8 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.dj = dj;
     P.dk = dk;
     P.epoch = W.epoch;
-    const int grid = ntasks < 2048 ? ntasks : 2048;
+    int grid = ntasks < 2048 ? ntasks : 2048;
+    if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
     hipLaunchKernelGGL(k_sweep_tile, dim3(grid), dim3(ST_THREADS), 0, st, P);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;

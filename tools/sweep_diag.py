@@ -30,27 +30,31 @@ ncell = np.prod(dims)
 print(f"cells {ncell}  sweep evals/cell/sweep = {p['sweep_evals']/ncell/16:.3f}")
 
 # per-task trace of one sweep (0 = first +++ sweep, 8 = first sweep of pass 2)
-for sw in (0, 8):
-    os.environ["SDFGEN_TRACE_SWEEP"] = str(sw)
-    _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_ARRAY3)
-    tr = _lib.debug_sweep_trace().astype(np.int64)
-    B = dims[1] - 1
-    C = dims[2] - 1
-    nJ = (B + 7) // 8
-    nK = (C + 7) // 8
-    order = [(J, d - J) for d in range(nJ + nK - 1) for J in range(nJ) if 0 <= d - J < nK]
-    tr = tr[: len(order)]
-    t0 = tr[:, 0].min()
-    start = (tr[:, 0] - t0) / 100.0  # us
-    end = (tr[:, 1] - t0) / 100.0
-    dur = end - start
-    pos = {jk: q for q, jk in enumerate(order)}
-    print(f"sweep {sw}: span {end.max():.1f} us; task duration min/med/max {dur.min():.1f}/{np.median(dur):.1f}/{dur.max():.1f} us")
-    for jk in [(0, 0), (1, 0), (0, 1), (1, 1), (2, 2), (4, 4), (8, 8), (16, 16), (nJ - 1, nK - 1)]:
-        if jk in pos:
-            q = pos[jk]
-            print(f"   task {jk}: start {start[q]:8.1f}  end {end[q]:8.1f}  dur {dur[q]:7.1f} us")
-    # how many tasks were active (started, not ended) over time
-    ts = np.linspace(0, end.max(), 12)
-    print("   active tasks over time:", [int(((start <= x) & (end > x)).sum()) for x in ts])
+for grid in ("", "512", "256"):
+    if grid:
+        os.environ["SDFGEN_TILE_GRID"] = grid
+    for sw in (0, 8):
+        os.environ["SDFGEN_TRACE_SWEEP"] = str(sw)
+        _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_ARRAY3)
+        p = _lib.last_profile()
+        tr = _lib.debug_sweep_trace().astype(np.int64)
+        B = dims[1] - 1
+        C = dims[2] - 1
+        nJ = (B + 7) // 8
+        nK = (C + 7) // 8
+        order = [(J, d - J) for d in range(nJ + nK - 1) for J in range(nJ) if 0 <= d - J < nK]
+        tr = tr[: len(order)]
+        t0 = tr[:, 0].min()
+        st = (tr - t0) / 100.0  # us: start, first step, mid, end
+        pos = {jk: q for q, jk in enumerate(order)}
+        nsteps = dims[0] - 1 + 14
+        half = nsteps / 2
+        print(f"grid={grid or 'auto'} sweep {sw}: sweep_ms {p['sweep_launch_ms'][sw]:.3f} span {st[:, 3].max():.1f} us")
+        for jk in [(0, 0), (1, 0), (2, 2), (4, 4), (6, 6), (8, 8), (12, 12), (16, 16), (24, 24), (nJ - 1, nK - 1)]:
+            if jk in pos:
+                q = pos[jk]
+                s0, s1, s2, s3 = st[q]
+                print(f"   task {jk}: start {s0:7.1f} first {s1:7.1f} mid {s2:7.1f} end {s3:7.1f}  "
+                      f"us/step 1st half {(s2 - s1) / half:5.2f}  2nd half {(s3 - s2) / half:5.2f}")
+    os.environ.pop("SDFGEN_TILE_GRID", None)
 del os.environ["SDFGEN_TRACE_SWEEP"]
