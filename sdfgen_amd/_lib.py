@@ -198,7 +198,7 @@ def debug_sweep_trace(device: int = 0, max_entries: int = 1 << 22) -> np.ndarray
     rc = lib.sdfgen_hip_debug_sweep_trace(device, out.ctypes.data_as(_P), max_entries, ctypes.byref(n))
     if rc != OK:
         raise RuntimeError("no sweep trace recorded (set SDFGEN_TRACE_SWEEP)")
-    return out[: n.value].reshape(-1, 4)
+    return out[: n.value].reshape(-1, 8)
 
 
 def debug_pit2d(pit: np.ndarray, device: int = 0) -> np.ndarray:

@@ -49,9 +49,14 @@ constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edg
 constexpr int ST_RO = 8;                      // own ring slots (steps)
 constexpr int ST_G = 4;                       // helper batch (steps / entries)
 constexpr int ST_RH = 32;                     // halo ring slots per stream (lead = RH-3 steps)
-constexpr int ST_THREADS = 128;               // compute wave + helper wave
-constexpr int ST_RING0 = 0;                                   // 4 slots x 64 columns
-constexpr int ST_HALO0 = ST_RING0 + 4 * ST_NCOL;              // 17 streams x RH
+constexpr int ST_NCW = 4;                     // compute waves per tile
+constexpr int ST_CLW = ST_T / ST_NCW;         // c-columns per compute wave (2)
+constexpr int ST_CPW = ST_T * ST_CLW;         // cells per compute wave (16)
+constexpr int ST_RR = 8;                      // neighbour ring slots (steps)
+constexpr int ST_LEAD = ST_RR - 4;            // max lead of wave w over wave w+1 (ring hazard)
+constexpr int ST_THREADS = 64 * (ST_NCW + 1); // compute waves + helper wave
+constexpr int ST_RING0 = 0;                                   // RR slots x 64 columns
+constexpr int ST_HALO0 = ST_RING0 + ST_RR * ST_NCOL;          // 17 streams x RH
 constexpr int ST_OWN0 = ST_HALO0 + ST_NSTREAM * ST_RH;        // RO slots x 64 columns
 constexpr int ST_ENTS = ST_OWN0 + ST_RO * ST_NCOL;
 constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
@@ -110,18 +115,17 @@ __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v
 __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
 {
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
-    __shared__ int s_pair[7 * ST_NCOL];     // compacted (entry << 9 | q << 6 | lane) evaluation list
-    __shared__ float s_d[7 * ST_NCOL];      // distance of candidate q for lane
+    __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
+    __shared__ float s_d[ST_NCW][7 * ST_CPW];      // per compute wave: distance of candidate q for lane
     __shared__ int s_own_fill;              // own entries ready for steps < s_own_fill
     __shared__ int s_halo_ready[ST_NSTREAM];  // halo entries < s_halo_ready[s] in LDS
-    __shared__ int s_progress;              // compute steps completed
+    __shared__ int s_prog[ST_NCW];          // steps completed by each compute wave
     __shared__ int s_abort;
     __shared__ int s_task;
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
     const int L = tid & 63;
-    const int bl = L & (ST_T - 1), cl = L >> 3;
     unsigned long long n_evals = 0, n_cpoll = 0, n_hpoll = 0, n_cpoll_own = 0;
 
     for (;;) {
@@ -133,23 +137,25 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
         const int J = JK.x, K = JK.y;
         const int b0 = J * ST_T, c0 = K * ST_T;
         const int nsteps = P.A + 2 * (ST_T - 1);
-        const int b = b0 + bl, c = c0 + cl;
-        const bool col = b < P.B && c < P.C;
 
-        // ---------------- task setup (both waves), then one barrier ----------------
-        if (wave == 0) {
-            // a = -1 entry of the own column (boundary plane, constant) -> ring slot 3
-            float4 v0, v1, v2;
-            int t = -1;
-            if (col) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
-            st_load_tri(P.soup, t, v0, v1, v2);
-            const int e = ST_RING0 + 3 * ST_NCOL + L;
-            s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
-            s_ent[3 * e + 1] = v1;
-            s_ent[3 * e + 2] = v2;
-            if (L == 0) {
+        // ---------------- task setup, then one barrier ----------------
+        if (wave < ST_NCW) {
+            if (L < ST_CPW) {
+                // a = -1 entry of each column (boundary plane, constant) -> ring slot 7
+                const int bl = L & (ST_T - 1), cl = ST_CLW * wave + (L >> 3);
+                const int b = b0 + bl, c = c0 + cl;
+                float4 v0, v1, v2;
+                int t = -1;
+                if (b < P.B && c < P.C) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
+                st_load_tri(P.soup, t, v0, v1, v2);
+                const int e = ST_RING0 + (ST_RR - 1) * ST_NCOL + cl * ST_T + bl;
+                s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
+                s_ent[3 * e + 1] = v1;
+                s_ent[3 * e + 2] = v2;
+            }
+            if (L == 0) s_prog[wave] = 0;
+            if (wave == 0 && L == 0) {
                 s_own_fill = 0;
-                s_progress = 0;
                 s_abort = 0;
             }
         } else if (L < ST_NSTREAM) {
@@ -170,15 +176,25 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
         }
         __syncthreads();
 
-        if (P.trace && tid == 0) P.trace[4 * task] = wall_clock64();
-        if (wave == 0) {
-            // ======================= compute wave =======================
+        if (P.trace && tid == 0) P.trace[8 * task] = wall_clock64();
+        if (wave < ST_NCW) {
+            // ======================= compute waves =======================
+            // Wave w owns the 16 columns cl in {2w, 2w+1}; lanes 0..15 are cells, all 64 lanes
+            // evaluate.  Wave w steps h only after wave w-1 finished step h-1 (its column
+            // cl-1 results) and at most 4 steps ahead of wave w+1 (8-slot ring).
+            const int w = wave;
+            const bool cell_lane = L < ST_CPW;
+            const int bl = L & (ST_T - 1), cl = ST_CLW * w + ((L >> 3) & 1);
+            const int col_id = cl * ST_T + bl;
+            const int b = b0 + bl, c = c0 + cl;
+            const bool col = cell_lane && b < P.B && c < P.C;
+            __builtin_amdgcn_s_setprio(2);
             int nb_base[7], nb_stride[7], nb_mask[7];
             {
                 auto ring = [&](int q, int lbl, int lcl) {
                     nb_base[q] = ST_RING0 + lcl * ST_T + lbl;
                     nb_stride[q] = ST_NCOL;
-                    nb_mask[q] = 3;
+                    nb_mask[q] = ST_RR - 1;
                 };
                 auto halo = [&](int q, int s) {
                     nb_base[q] = ST_HALO0 + s * ST_RH;
@@ -196,19 +212,27 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 else { halo(5, ST_T + bl - 1); halo(6, ST_T + bl - 1); }
             }
             unsigned polls = 0;
+            unsigned long long t_wait = 0, w_own = 0, w_halo = 0, t_comp = 0, c_comp = 0;   // trace-only
             for (int h = 0; h < nsteps; ++h) {
                 const int a = h - bl - cl;
                 const bool act = col && a >= 0 && a < P.A;
-                // ---- wait until the helper has landed everything this step reads ----
+                // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
+                unsigned long long tw0 = 0;
                 for (;;) {
                     const bool own_ok = lds_ld(&s_own_fill) > h;
                     bool ok = own_ok;
+                    if (w > 0 && lds_ld(&s_prog[w - 1]) < h) ok = false;
+                    if (w < ST_NCW - 1 && lds_ld(&s_prog[w + 1]) < h - ST_LEAD) ok = false;
                     if (act) {
                         if (bl == 0 && lds_ld(&s_halo_ready[cl]) <= a) ok = false;
                         if (cl == 0 && lds_ld(&s_halo_ready[ST_T + bl]) <= a) ok = false;
                         if (bl == 0 && cl == 0 && lds_ld(&s_halo_ready[2 * ST_T]) <= a) ok = false;
                     }
                     if (__all(ok)) break;
+                    if (P.trace && tw0 == 0) {
+                        tw0 = wall_clock64();
+                        if (!__all(own_ok)) ++w_own; else ++w_halo;
+                    }
                     ++n_cpoll;
                     if (!__all(own_ok)) ++n_cpoll_own;
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
@@ -219,14 +243,17 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     __builtin_amdgcn_s_sleep(1);
                 }
                 asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
+                if (tw0) t_wait += wall_clock64() - tw0;
                 if (h >= nsteps) break;
+                const unsigned long long tc0 = P.trace ? wall_clock64() : 0ull;
+                const unsigned long long cc0 = P.trace ? clock64() : 0ull;
                 polls = 0;
                 // ---- candidates: the 7 upwind labels minus exact duplicates ----
                 float phi = 0.f;
                 int ct = -1, ct_orig = -1, win = -1;
                 int lab[7], ent[7];
                 unsigned fmask = 0;
-                const int e_own = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + L;
+                const int e_own = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id;
                 if (act) {
                     const float4 o0 = s_ent[3 * e_own], o1 = s_ent[3 * e_own + 1];
                     ct = __float_as_int(o0.w);
@@ -255,32 +282,29 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     if (f) {
                         const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        s_pair[pos] = (ent[q] << 9) | (q << 6) | L;
+                        s_pair[w][pos] = (ent[q] << 9) | (q << 6) | L;
                     }
                     total += (int)__popcll(m);
                 }
-                // ---- evaluate: one pair per lane, or two independent chains per lane ----
-                if (total <= ST_NCOL) {
-                    if (L < total) {
-                        const int p1 = s_pair[L];
-                        const int l1 = p1 & 63, e1 = p1 >> 9;
-                        const f3 g1 = st_gx(P, h - (l1 & 7) - (l1 >> 3), b0 + (l1 & 7), c0 + (l1 >> 3));
-                        s_d[((p1 >> 6) & 7) * ST_NCOL + l1] =
-                            ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
-                    }
-                } else {
-                    for (int k = L; k < total; k += 128) {
-                        const int p1 = s_pair[k];
-                        const bool has2 = k + 64 < total;
-                        const int p2 = has2 ? s_pair[k + 64] : p1;
-                        const int l1 = p1 & 63, l2 = p2 & 63;
-                        const int e1 = p1 >> 9, e2 = p2 >> 9;
-                        const f3 g1 = st_gx(P, h - (l1 & 7) - (l1 >> 3), b0 + (l1 & 7), c0 + (l1 >> 3));
-                        const f3 g2 = st_gx(P, h - (l2 & 7) - (l2 >> 3), b0 + (l2 & 7), c0 + (l2 >> 3));
+                // ---- evaluate (<= 112 pairs): one per lane, a second chain only if needed ----
+                for (int k = L; k < total; k += 128) {
+                    const int p1 = s_pair[w][k];
+                    const bool has2 = k + 64 < total;
+                    const int l1 = p1 & 63, e1 = p1 >> 9;
+                    const f3 g1 = st_gx(P, h - (l1 & 7) - (ST_CLW * w + (l1 >> 3)), b0 + (l1 & 7),
+                                        c0 + ST_CLW * w + (l1 >> 3));
+                    if (__any(has2)) {
+                        const int p2 = has2 ? s_pair[w][k + 64] : p1;
+                        const int l2 = p2 & 63, e2 = p2 >> 9;
+                        const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
+                                            c0 + ST_CLW * w + (l2 >> 3));
                         const float d1 = ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
                         const float d2 = ptd_nb(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
-                        s_d[((p1 >> 6) & 7) * ST_NCOL + l1] = d1;
-                        if (has2) s_d[((p2 >> 6) & 7) * ST_NCOL + l2] = d2;
+                        s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
+                        if (has2) s_d[w][((p2 >> 6) & 7) * ST_CPW + l2] = d2;
+                    } else {
+                        s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] =
+                            ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
@@ -289,7 +313,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         if ((fmask >> q) & 1u) {
-                            const float d = s_d[q * ST_NCOL + L];
+                            const float d = s_d[w][q * ST_CPW + L];
                             if (d < phi) {
                                 phi = d;
                                 ct = lab[q];
@@ -300,7 +324,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     const int src = win < 0 ? e_own : win;
                     const float4 w0 = s_ent[3 * src];
                     const float4 w1 = s_ent[3 * src + 1], w2 = s_ent[3 * src + 2];
-                    const int slot = ST_RING0 + (a & 3) * ST_NCOL + L;
+                    const int slot = ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id;
                     s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __int_as_float(ct));
                     s_ent[3 * slot + 1] = w1;
                     s_ent[3 * slot + 2] = w2;
@@ -314,12 +338,27 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                         __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                 }
+                if (P.trace) {
+                    t_comp += wall_clock64() - tc0;
+                    c_comp += clock64() - cc0;
+                }
                 lds_drain();
-                if (L == 0) lds_st(&s_progress, h + 1);
-                if (P.trace && L == 0 && (h == 0 || h == nsteps / 2)) P.trace[4 * task + (h == 0 ? 1 : 2)] = wall_clock64();
+                if (L == 0) lds_st(&s_prog[w], h + 1);
+                if (P.trace && w == 0 && L == 0 && (h == 0 || h == nsteps / 2))
+                    P.trace[8 * task + (h == 0 ? 1 : 2)] = wall_clock64();
             }
-            if (P.trace && L == 0) P.trace[4 * task + 3] = wall_clock64();
+            __builtin_amdgcn_s_setprio(0);
+            if (P.trace && w == 0 && L == 0) {
+                P.trace[8 * task + 3] = wall_clock64();
+                P.trace[8 * task + 4] = t_wait;
+                P.trace[8 * task + 5] = w_own + (w_halo << 32);
+                P.trace[8 * task + 6] = c_comp;
+                P.trace[8 * task + 7] = t_comp;
+            }
         } else {
+            const int bl = L & (ST_T - 1), cl = L >> 3;   // helper lane L prefetches column (bl, cl)
+            const int b = b0 + bl, c = c0 + cl;
+            const bool col = b < P.B && c < P.C;
             // ======================= helper wave =======================
             // stream geometry (lanes < 17)
             const bool hlane = L < ST_NSTREAM;
@@ -355,7 +394,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, 0, 0);
             unsigned idle = 0;
             for (;;) {
-                const int prog = lds_ld(&s_progress);
+                const int prog = lds_ld(&s_prog[ST_NCW - 1]);   // the last compute wave is the slowest
                 if (lds_ld(&s_abort)) break;
                 // The batch-A loads were issued one iteration ago: wait for them once, and hand
                 // the registers back through the asm so the compiler does not track them as
@@ -398,13 +437,14 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             (g) >= hcB ? P.cell + dummy : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g)); \
         qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                      \
     }
-                unsigned long long n0 = ~0ull, n1 = ~0ull, n2 = ~0ull, n3 = ~0ull, m0 = 0, m1 = 0, m2 = 0, m3 = 0;
-                if (__any(gB > 0 || hcB > 0)) {   // wave-uniform: idle helpers issue nothing
-                    ST_ISSUE(0, n0, m0)
-                    ST_ISSUE(1, n1, m1)
-                    ST_ISSUE(2, n2, m2)
-                    ST_ISSUE(3, n3, m3)
-                }
+                // Always issued (a fixed count keeps the waits below precise); slots with nothing
+                // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
+                // not flood the fabric with granule polls.
+                unsigned long long n0, n1, n2, n3, m0, m1, m2, m3;
+                ST_ISSUE(0, n0, m0)
+                ST_ISSUE(1, n1, m1)
+                ST_ISSUE(2, n2, m2)
+                ST_ISSUE(3, n3, m3)
                 // ---- land batch A in LDS, then publish readiness ----
 #define ST_LAND(g, cg, qg)                                                                             \
     if (ST_OWN_OK(g)) {                                                                                \
@@ -544,7 +584,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.stats = W.count ? W.stats : nullptr;
     P.trace = nullptr;
     if (W.trace_sweep >= 0 && W.trace_sweep == W.cur_sweep) {
-        if (st_grow(&W.trace, &W.cap_trace, 4 * (size_t)ntasks)) return fail(-5, "trace");
+        if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks)) return fail(-5, "trace");
         P.trace = W.trace;
     }
     P.ox = origin[0];

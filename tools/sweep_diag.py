@@ -30,7 +30,7 @@ ncell = np.prod(dims)
 print(f"cells {ncell}  sweep evals/cell/sweep = {p['sweep_evals']/ncell/16:.3f}")
 
 # per-task trace of one sweep (0 = first +++ sweep, 8 = first sweep of pass 2)
-for grid in ("", "512", "256"):
+for grid in ("",):
     if grid:
         os.environ["SDFGEN_TILE_GRID"] = grid
     for sw in (0, 8):
@@ -45,7 +45,10 @@ for grid in ("", "512", "256"):
         order = [(J, d - J) for d in range(nJ + nK - 1) for J in range(nJ) if 0 <= d - J < nK]
         tr = tr[: len(order)]
         t0 = tr[:, 0].min()
-        st = (tr - t0) / 100.0  # us: start, first step, mid, end
+        st = (tr[:, :4] - t0) / 100.0  # us: start, first step, mid, end
+        wt = tr[:, 4] / 100.0          # us waiting in polls
+        wo, wh = tr[:, 5] & 0xffffffff, tr[:, 5] >> 32   # steps that waited on own data / on halo
+        clk = tr[:, 6] / np.maximum(tr[:, 7], 1) / 10.0  # shader clock (GHz) during compute
         pos = {jk: q for q, jk in enumerate(order)}
         nsteps = dims[0] - 1 + 14
         half = nsteps / 2
@@ -55,6 +58,8 @@ for grid in ("", "512", "256"):
                 q = pos[jk]
                 s0, s1, s2, s3 = st[q]
                 print(f"   task {jk}: start {s0:7.1f} first {s1:7.1f} mid {s2:7.1f} end {s3:7.1f}  "
-                      f"us/step 1st half {(s2 - s1) / half:5.2f}  2nd half {(s3 - s2) / half:5.2f}")
+                      f"us/step 1st half {(s2 - s1) / half:5.2f}  2nd half {(s3 - s2) / half:5.2f}  "
+                      f"wait {wt[q]:7.1f} us (own {wo[q]}, halo {wh[q]} steps)  "
+                      f"busy/step {((s3 - s0) - wt[q]) / nsteps:5.2f}  compute/step {tr[q, 7] / 100.0 / nsteps:5.2f}  clk {clk[q]:.2f} GHz")
     os.environ.pop("SDFGEN_TILE_GRID", None)
 del os.environ["SDFGEN_TRACE_SWEEP"]
