@@ -66,45 +66,46 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    import torch
-    import torch.distributed as dist
-
-    from sdfgen_amd import _lib, meshgen
-
+    dist = None
     if world > 1:
+        # Control plane only (barrier + max of the wall time): gloo on the host.  The data
+        # path has no collective -- each rank runs an independent job on its own GPU.
+        # torch is imported BEFORE the backend so one HIP runtime serves both.
+        import torch
+        import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device(f"cuda:{local_rank}")
+        dist.init_process_group("gloo")
 
+    from sdfgen_amd import _hiprt, _lib, meshgen
+
+    _hiprt.set_device(local_rank)
     v, t, o, dx, dims = meshgen.workload(args.workload)
     ni, nj, nk = dims
     ncell = ni * nj * nk
-    dv = torch.from_numpy(v).to(dev)
-    dt = torch.from_numpy(t.view(np.int32)).to(dev)
-    out = torch.empty(ncell, dtype=torch.float32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    dv = _hiprt.DeviceBuffer.from_array(v)
+    dt = _hiprt.DeviceBuffer.from_array(t)
+    out = _hiprt.DeviceBuffer(ncell * 4)
 
     def step():
-        _lib.make_level_set3_device(local_rank, dt.data_ptr(), t.shape[0], dv.data_ptr(), v.shape[0], o, dx,
-                                    ni, nj, nk, 1, _lib.LAYOUT_ARRAY3, out.data_ptr(), stream.cuda_stream)
+        _lib.make_level_set3_device(local_rank, dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx,
+                                    ni, nj, nk, 1, _lib.LAYOUT_ARRAY3, out.ptr, 0)
         return _lib.last_profile()
 
     def barrier():
-        if world > 1:
+        if dist is not None:
             dist.barrier()
 
     for _ in range(args.warmup):
         step()
+    _hiprt.synchronize()
     barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     profs = [step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    barrier()
+    _hiprt.synchronize()
     el = time.perf_counter() - t0
-    if world > 1:
-        x = torch.tensor([el], dtype=torch.float64, device=dev)
+    barrier()
+    if dist is not None:
+        x = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(x, op=dist.ReduceOp.MAX)
         el = float(x.item())
 
@@ -126,7 +127,7 @@ def main():
         if os.path.exists(hp):
             rec = json.load(open(hp)).get(args.workload)
             if rec:
-                got = out.cpu().numpy()
+                got = out.download(np.float32, ncell)
                 ok = hashlib.sha256(got.astype("<f4").tobytes()).hexdigest() == rec["sha256_phi"]
                 parity = "bit-exact vs reference (sha256 of phi)" if ok else "MISMATCH vs reference sha256"
 

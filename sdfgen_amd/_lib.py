@@ -14,7 +14,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsdfgen_hip.so")
+LIB_PATH = os.environ.get("SDFGEN_LIB_OVERRIDE") or os.path.join(_HERE, "libsdfgen_hip.so")   # override: diagnostics only
 
 OK, EINVAL, EINDEX, ENODEV, ERUNTIME, ENOMEM = 0, -1, -2, -3, -4, -5
 LAYOUT_ARRAY3, LAYOUT_KFAST = 0, 1

@@ -420,11 +420,15 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->wf.trace_sweep = tr ? atoi(tr) : -1;
         const char *gr = getenv("SDFGEN_TILE_GRID");     // diagnostics: cap on resident workgroups
         ws->wf.grid_override = gr ? atoi(gr) : 0;
+        const char *ld = getenv("SDFGEN_TILE_LEAD");      // diagnostics: inter-wave lead
+        ws->wf.lead_override = ld ? atoi(ld) : -1;
         if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 32, st));
     }
+    const char *nsw_env = getenv("SDFGEN_DEBUG_NSWEEPS");   // diagnostics: stop after n sweeps
+    const int nsweeps = nsw_env ? atoi(nsw_env) : 16;
     for (int s = 0; s < 16; ++s) {
         HIPCHK(hipEventRecord(ev[3 + s], st));
-        if (!do_sweep) continue;
+        if (!do_sweep || s >= nsweeps) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
         if (impl == 1) {
             ws->wf.cur_sweep = s;

@@ -48,8 +48,14 @@ constexpr int ST_NCOL = ST_T * ST_T;          // 64 columns = one wave
 constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edge (8), corner
 constexpr int ST_RO = 8;                      // own ring slots (steps)
 constexpr int ST_G = 4;                       // helper batch (steps / entries)
-constexpr int ST_RH = 32;                     // halo ring slots per stream (lead = RH-3 steps)
-constexpr int ST_NCW = 4;                     // compute waves per tile
+#ifndef ST_RH_DEF
+#define ST_RH_DEF 32
+#endif
+#ifndef ST_NCW_DEF
+#define ST_NCW_DEF 4
+#endif
+constexpr int ST_RH = ST_RH_DEF;                     // halo ring slots per stream (lead = RH-3 steps)
+constexpr int ST_NCW = ST_NCW_DEF;                     // compute waves per tile
 constexpr int ST_CLW = ST_T / ST_NCW;         // c-columns per compute wave (2)
 constexpr int ST_CPW = ST_T * ST_CLW;         // cells per compute wave (16)
 constexpr int ST_RR = 8;                      // neighbour ring slots (steps)
@@ -76,6 +82,7 @@ struct StParams {
     int A, B, C, nJ, nK, ntasks;
     int di, dj, dk;
     unsigned epoch;
+    int lead;                     // max steps wave w may run ahead of wave w+1 (<= ST_LEAD)
 };
 
 __device__ __forceinline__ size_t st_phys(const StParams &P, int a, int b, int c)
@@ -100,6 +107,13 @@ __device__ __forceinline__ int lds_ld(const int *p) { return __hip_atomic_load(p
 __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // all of this wave's LDS writes have executed before anything after this point
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+#ifdef ST_DEBUG_TAGS
+// debug builds: the spare .w of an entry's third float4 carries (kind, column/stream, a+1)
+#define ST_TAGF(kind, id, a) __int_as_float(((kind) << 28) | ((id) << 16) | (((a) + 1) & 0xffff))
+#else
+#define ST_TAGF(kind, id, a) 0.f
+#endif
 
 __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v0, float4 &v1, float4 &v2)
 {
@@ -151,7 +165,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 const int e = ST_RING0 + (ST_RR - 1) * ST_NCOL + cl * ST_T + bl;
                 s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
                 s_ent[3 * e + 1] = v1;
-                s_ent[3 * e + 2] = v2;
+                s_ent[3 * e + 2] = make_float4(v2.x, v2.y, v2.z, ST_TAGF(1, cl * ST_T + bl, -1));
             }
             if (L == 0) s_prog[wave] = 0;
             if (wave == 0 && L == 0) {
@@ -171,7 +185,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             const int e = ST_HALO0 + L * ST_RH + (ST_RH - 1);
             s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
             s_ent[3 * e + 1] = v1;
-            s_ent[3 * e + 2] = v2;
+            s_ent[3 * e + 2] = make_float4(v2.x, v2.y, v2.z, ST_TAGF(3, L, -1));
             s_halo_ready[L] = valid ? 0 : P.A;
         }
         __syncthreads();
@@ -184,7 +198,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             // cl-1 results) and at most 4 steps ahead of wave w+1 (8-slot ring).
             const int w = wave;
             const bool cell_lane = L < ST_CPW;
-            const int bl = L & (ST_T - 1), cl = ST_CLW * w + ((L >> 3) & 1);
+            const int bl = L & (ST_T - 1), cl = ST_CLW * w + ((L >> 3) & (ST_CLW - 1));
             const int col_id = cl * ST_T + bl;
             const int b = b0 + bl, c = c0 + cl;
             const bool col = cell_lane && b < P.B && c < P.C;
@@ -222,7 +236,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     const bool own_ok = lds_ld(&s_own_fill) > h;
                     bool ok = own_ok;
                     if (w > 0 && lds_ld(&s_prog[w - 1]) < h) ok = false;
-                    if (w < ST_NCW - 1 && lds_ld(&s_prog[w + 1]) < h - ST_LEAD) ok = false;
+                    if (w < ST_NCW - 1 && lds_ld(&s_prog[w + 1]) < h - P.lead) ok = false;
                     if (act) {
                         if (bl == 0 && lds_ld(&s_halo_ready[cl]) <= a) ok = false;
                         if (cl == 0 && lds_ld(&s_halo_ready[ST_T + bl]) <= a) ok = false;
@@ -265,6 +279,27 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                         ent[q] = nb_base[q] + (aq & nb_mask[q]) * nb_stride[q];
                         lab[q] = __float_as_int(s_ent[3 * ent[q]].w);
                     }
+#ifdef ST_DEBUG_TAGS
+                    {
+                        const int og = __float_as_int(s_ent[3 * e_own + 2].w);
+                        const int oe = __float_as_int(ST_TAGF(2, col_id, a));
+                        if (og != oe && atomicAdd(P.err + 2, 1) < 24)
+                            printf("TAG own J=%d K=%d w=%d h=%d bl=%d cl=%d a=%d want %08x got %08x own_fill=%d prog=%d,%d,%d,%d\n",
+                                   J, K, w, h, bl, cl, a, oe, og, s_own_fill, s_prog[0], s_prog[ST_NCW > 1 ? 1 : 0],
+                                   s_prog[ST_NCW > 2 ? 2 : 0], s_prog[ST_NCW - 1]);
+                        for (int q = 0; q < 7; ++q) {
+                            const int aq = (q & 1) == 0 ? a - 1 : a;
+                            const bool isring = nb_stride[q] == ST_NCOL;
+                            const int id = isring ? nb_base[q] - ST_RING0 : (nb_base[q] - ST_HALO0) / ST_RH;
+                            const int want = __float_as_int(ST_TAGF(isring ? 1 : 3, id, aq));
+                            const int got = __float_as_int(s_ent[3 * ent[q] + 2].w);
+                            if (want != got && atomicAdd(P.err + 2, 1) < 24)
+                                printf("TAG nb J=%d K=%d w=%d h=%d bl=%d cl=%d a=%d q=%d want %08x got %08x prog=%d,%d,%d,%d hr=%d\n",
+                                       J, K, w, h, bl, cl, a, q, want, got, s_prog[0], s_prog[ST_NCW > 1 ? 1 : 0],
+                                       s_prog[ST_NCW > 2 ? 2 : 0], s_prog[ST_NCW - 1], isring ? -1 : s_halo_ready[id]);
+                        }
+                    }
+#endif
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         bool skip = (lab[q] < 0) || (lab[q] == ct_orig);
@@ -327,7 +362,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     const int slot = ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id;
                     s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __int_as_float(ct));
                     s_ent[3 * slot + 1] = w1;
-                    s_ent[3 * slot + 2] = w2;
+                    s_ent[3 * slot + 2] = make_float4(w2.x, w2.y, w2.z, ST_TAGF(1, col_id, a));
                     if (win >= 0)
                         P.cell[st_phys(P, a, b, c)] = ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
                     const unsigned long long gran = ((unsigned long long)P.epoch << 32) | (uint32_t)ct;
@@ -394,7 +429,11 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, 0, 0);
             unsigned idle = 0;
             for (;;) {
-                const int prog = lds_ld(&s_prog[ST_NCW - 1]);   // the last compute wave is the slowest
+                // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
+                // may finish step h while wave w-1 is still on step h (it needs only h-1 of it).
+                int prog = lds_ld(&s_prog[0]);
+#pragma unroll
+                for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_prog[w]));
                 if (lds_ld(&s_abort)) break;
                 // The batch-A loads were issued one iteration ago: wait for them once, and hand
                 // the registers back through the asm so the compiler does not track them as
@@ -451,13 +490,13 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
         const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + L;                   \
         s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __int_as_float((int)(uint32_t)(cg)));   \
         s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
-        s_ent[3 * e_ + 2] = oc##g;                                                                     \
+        s_ent[3 * e_ + 2] = make_float4(oc##g.x, oc##g.y, oc##g.z, ST_TAGF(2, L, fA + (g) - bl - cl)); \
     }                                                                                                  \
     if ((g) < hp) {                                                                                    \
         const int e_ = ST_HALO0 + L * ST_RH + ((hA + (g)) & (ST_RH - 1));                              \
         s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __int_as_float((int)(uint32_t)(qg)));   \
         s_ent[3 * e_ + 1] = hb##g;                                                                     \
-        s_ent[3 * e_ + 2] = hc##g;                                                                     \
+        s_ent[3 * e_ + 2] = make_float4(hc##g.x, hc##g.y, hc##g.z, ST_TAGF(3, L, hA + (g)));        \
     }
                 ST_LAND(0, c0, q0)
                 ST_LAND(1, c1, q1)
@@ -510,6 +549,7 @@ struct TileSweepWorkspace {
     int trace_sweep = -1;      // which sweep (0..15) to trace, -1 = none
     int cur_sweep = 0;
     int grid_override = 0;     // diagnostics: cap on resident workgroups
+    int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
     size_t cap_hb = 0, cap_hc = 0;
     int2 *tasks = nullptr;
     size_t cap_tasks = 0;
@@ -604,6 +644,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.dj = dj;
     P.dk = dk;
     P.epoch = W.epoch;
+    P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
     hipLaunchKernelGGL(k_sweep_tile, dim3(grid), dim3(ST_THREADS), 0, st, P);
