@@ -95,12 +95,17 @@ typedef struct sdfgen_hip_profile {
     double sign_ms;           /* sign pass + output layout */
     double sweep_launch_ms[16];  /* per (pass, direction) sweep */
     int sweep_launches;       /* kernel launches issued for the sweeps */
-    int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined 8x8-tile column wavefront */
+    int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined 8x8-tile column wavefront,
+                                 2 = tile wavefront for the first pass + Jacobi/repair for sparse sweeps */
     uint64_t band_evals;      /* point-triangle evaluations in the band phase */
     uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless SDFGEN_COUNT_EVALS is set) */
     uint64_t sweep_stalls;    /* compute-wave polls that found a hand-off not yet landed (same) */
     uint64_t helper_polls;    /* helper-wave polls that found nothing to fetch (same) */
     uint64_t own_waits;       /* compute-wave polls waiting on the column prefetch (same) */
+    int sparse_sweeps;        /* sweeps run as Jacobi + change-driven repair */
+    int sparse_first;         /* index of the first such sweep (16 = none) */
+    uint64_t sparse_rechecks; /* cell re-evaluations in the repair kernels (all sparse sweeps) */
+    uint64_t sparse_claims;   /* rechecks run depth-first by the lane that requested them */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

@@ -52,6 +52,10 @@ class Profile(ctypes.Structure):
         ("sweep_stalls", ctypes.c_uint64),
         ("helper_polls", ctypes.c_uint64),
         ("own_waits", ctypes.c_uint64),
+        ("sparse_sweeps", ctypes.c_int),
+        ("sparse_first", ctypes.c_int),
+        ("sparse_rechecks", ctypes.c_uint64),
+        ("sparse_claims", ctypes.c_uint64),
     ]
 
     def as_dict(self):

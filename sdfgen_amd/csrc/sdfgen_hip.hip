@@ -27,6 +27,7 @@
 #include "geom.hpp"
 #include "sdfgen_hip.h"
 #include "sweep_tile.hpp"
+#include "sweep_sparse.hpp"
 
 using namespace sdfhip;
 
@@ -297,6 +298,8 @@ struct Workspace {
     hipStream_t stream = nullptr;
     u64 *cell = nullptr;
     uint32_t *cnt = nullptr;
+    unsigned char *lc = nullptr;   // last sweep (+1) that changed each cell's label (sparse sweeps)
+    size_t cap_lc = 0;
     float4 *soup = nullptr;
     uint32_t *tri = nullptr;
     float *xyz = nullptr;
@@ -307,6 +310,7 @@ struct Workspace {
     bool ev_ok = false;
     std::mutex mu;
     TileSweepWorkspace wf;
+    SparseSweepWorkspace sp;
 };
 
 std::mutex g_mu;
@@ -426,13 +430,39 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     }
     const char *nsw_env = getenv("SDFGEN_DEBUG_NSWEEPS");   // diagnostics: stop after n sweeps
     const int nsweeps = nsw_env ? atoi(nsw_env) : 16;
+    // Sweeps from `sparse_first` on run as Jacobi + repair (sweep_sparse.hpp): in the second
+    // pass only ~0.05 % of the labels change.  SDFGEN_SPARSE_FROM overrides (16 = never).
+    int sparse_first = 16;
+    if (impl == 1 && sparse_sweep_supported(n, ni, nj, nk)) {
+        const char *e = getenv("SDFGEN_SPARSE_FROM");
+        sparse_first = e ? std::max(0, std::min(16, atoi(e))) : 8;
+    }
+    int sparse_sweeps = 0;
+    {
+        const char *e = getenv("SDFGEN_SPARSE_WORKERS");   // diagnostics: repair-kernel workgroups
+        ws->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
+    }
+    if (sparse_first < 16) {
+        if ((rc = grow(&ws->lc, &ws->cap_lc, n, err))) return rc;
+        HIPCHK(hipMemsetAsync(ws->lc, 0, n, st));
+    }
+    unsigned char *lc = sparse_first < 16 ? ws->lc : nullptr;
+    if (ws->wf.ctrl) HIPCHK(hipMemsetAsync(ws->wf.ctrl + 1, 0, sizeof(int), st));   // error bits of this call
+    if (sparse_first < 16 && ws->sp.ctl) HIPCHK(hipMemsetAsync(ws->sp.ctl, 0, SP_NCTL * sizeof(u64), st));
     for (int s = 0; s < 16; ++s) {
         HIPCHK(hipEventRecord(ev[3 + s], st));
         if (!do_sweep || s >= nsweeps) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
+        if (impl == 1 && s >= sparse_first) {
+            if ((rc = sparse_sweep(ws->sp, st, ws->soup, &ws->cell, &ws->cap_cell, lc, origin, dx, ni, nj, nk, s)))
+                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU sparse sweep setup failed");
+            launches += 2;
+            ++sparse_sweeps;
+            continue;
+        }
         if (impl == 1) {
             ws->wf.cur_sweep = s;
-            if ((rc = tile_sweep(ws->wf, st, ws->soup, ws->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
+            if ((rc = tile_sweep(ws->wf, st, ws->soup, ws->cell, lc, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
                                       err.len)))
                 return rc;
             ++launches;
@@ -459,9 +489,11 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     }
     HIPCHK(hipEventRecord(ev[20], st));
     int flag = 0, wf_err = 0;
-    unsigned long long evals = 0, wf_stats[4] = {0, 0, 0, 0};
+    unsigned long long evals = 0, wf_stats[4] = {0, 0, 0, 0}, sp_ctl[SP_NCTL] = {};
+    if (sparse_sweeps)
+        HIPCHK(hipMemcpyAsync(sp_ctl, ws->sp.ctl, sizeof(sp_ctl), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    if (impl == 1) {
+    if (impl == 1 && ws->wf.ctrl) {
         HIPCHK(hipMemcpyAsync(&wf_err, ws->wf.ctrl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
         if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, 32, hipMemcpyDeviceToHost, st));
     }
@@ -493,11 +525,17 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sweep_stalls = wf_stats[1];
     p.helper_polls = wf_stats[2];
     p.own_waits = wf_stats[3];
+    p.sparse_sweeps = sparse_sweeps;
+    p.sparse_first = sparse_sweeps ? sparse_first : 16;
+    p.sparse_rechecks = sp_ctl[SP_RUNS];
+    p.sparse_claims = sp_ctl[SP_ENQ];
+    if (sparse_sweeps) p.sweep_impl = 2;
     {
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;
     }
     if (wf_err) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
+    if (sp_ctl[SP_ERR]) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sparse sweep watchdog fired (work list stalled)");
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
                              (unsigned long long)nvert);
     return 0;
@@ -595,6 +633,7 @@ int sdfgen_hip_release(void)
     for (Workspace *w : g_ws) {
         hipSetDevice(w->device);
         hipFree(w->cell);
+        hipFree(w->lc);
         hipFree(w->cnt);
         hipFree(w->soup);
         hipFree(w->tri);
@@ -602,6 +641,7 @@ int sdfgen_hip_release(void)
         hipFree(w->err_flag);
         hipFree(w->evals);
         tile_sweep_release(w->wf);
+        sparse_sweep_release(w->sp);
         for (auto &e : w->ev) hipEventDestroy(e);
         hipStreamDestroy(w->stream);
         delete w;

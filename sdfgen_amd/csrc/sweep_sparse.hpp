@@ -1,0 +1,395 @@
+// sweep_sparse.hpp -- a sweep direction in which few labels change, computed as a
+// parallel Jacobi evaluation followed by an exact, change-driven repair.
+//
+// Why this is exact.  In one reference sweep (cpu_lib/makelevelset3.cpp:130-151) a
+// cell's result depends on its own value from before the sweep (S) and on the CURRENT
+// labels of its 7 upwind neighbours -- never on their phi (:94-99).  Write the sweep
+// as x_c = f(S_c, labels(x_upwind(c))).  The upwind relation is acyclic, so this system
+// has exactly one solution: the Gauss-Seidel result.  We
+//   1. evaluate J_c = f(S_c, labels(S_upwind(c))) for every cell at once (k_sp_jacobi);
+//      J_c is already the answer for every cell none of whose upwind neighbours changes;
+//   2. repair: whenever a cell's label differs from its S label (or later changes
+//      again), each downstream neighbour is re-evaluated with the labels current at
+//      that time (k_sp_recheck).  Every label change is followed by a re-evaluation
+//      that reads it, so when the work list drains every cell satisfies its equation,
+//      i.e. X is the unique solution = the reference's bits, in any processing order.
+// In the second pass of sweeps only ~0.02-0.07 % of the cells change (256^3, DESIGN.md
+// §4), so step 2 touches a few thousand cells instead of walking the whole
+// dependency chain.
+//
+// Concurrency protocol (one device, all memory ops at agent scope so the 8 XCD L2s
+// agree):
+//   * req[c] counts outstanding recheck requests.  A request that moves it 0 -> 1 owns
+//     the cell: it is queued (or run directly by the requester, depth-first).  The
+//     runner reads r = req[c], evaluates, and retires r; if more requests arrived
+//     meanwhile it evaluates again.  So a cell is never evaluated by two lanes at once
+//     and no request is lost.
+//   * a new label is published (its store completes) before the requests it triggers;
+//     a runner reads labels only after the request it retires was observed: the first
+//     evaluation retires just the request that handed it the cell (written after the
+//     label that caused it), and every further round retires what its atomicSub saw.
+//   * ctl[PENDING] counts queued or running work items; workers leave when it is 0.
+// Every spin is bounded (watchdog -> error bit, reported by the host).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "geom.hpp"
+
+namespace sdfhip {
+
+enum { SP_TAIL = 0, SP_HEAD = 1, SP_PENDING = 2, SP_ERR = 3, SP_ENQ = 4, SP_RUNS = 5, SP_NCTL = 8 };
+constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
+constexpr int SP_WORKERS = 512;              // max one-wave workgroups of the repair kernel
+constexpr int SP_WORKERS_DEFAULT = 128;
+
+// the reference's 8 sweep directions in pass order (cpu_lib/makelevelset3.cpp:243-291)
+constexpr int SP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
+                               {+1, -1, +1}, {-1, +1, -1}, {+1, -1, -1}, {-1, +1, +1}};
+
+struct SpParams {
+    const float4 *soup;                // 3 float4 per triangle
+    const unsigned long long *S;       // (phi bits << 32) | label before the sweep, i-fastest
+    unsigned long long *X;             // result of the sweep
+    unsigned *req;                     // per-cell recheck requests (zero between sweeps)
+    unsigned *queue;                   // ring of cell+1 (0 = empty)
+    unsigned long long *ctl;           // SP_* counters
+    unsigned long long cap;            // ring slots
+    unsigned long long n;              // cells
+    unsigned char *lc;                 // per cell: 0 = label from the band, s+1 = last changed in sweep s
+    float ox, oy, oz, dx;
+    int ni, nj, nk;
+    int di, dj, dk;
+    int sweep;                         // index (0..15) of this sweep
+    int seen[7];                       // per neighbour slot q: s'+1 of the last earlier sweep in which
+                                       // an interior cell examined that neighbour (-1: none)
+};
+
+__device__ __forceinline__ unsigned long long sp_ld64(const unsigned long long *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sp_st64(unsigned long long *p, unsigned long long v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Every shared word of the repair pass (X, req, queue, ctl) is accessed with agent-scope
+// (sc1) atomics, which are coherent across the XCD L2s; ordering between two of them
+// only needs the first to have completed before the second issues.  That is a
+// vmcnt wait -- not __threadfence(), whose L2 write-back is for plain stores.
+__device__ __forceinline__ void sp_order() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ unsigned sp_ld32(const unsigned *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sp_st32(unsigned *p, unsigned v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// cell inside the reference's loop range for this direction (i0..i1 of :243-291)
+__device__ __forceinline__ bool sp_in(const SpParams &P, int i, int j, int k)
+{
+    return (P.di > 0 ? i >= 1 : i <= P.ni - 2) && (P.dj > 0 ? j >= 1 : j <= P.nj - 2) &&
+           (P.dk > 0 ? k >= 1 : k <= P.nk - 2);
+}
+
+// f(own, upwind labels) in the reference's check order (:143-149): strict '<', first
+// minimum wins; labels equal to the cell's own original label or to an earlier
+// candidate are skipped (their distance cannot win -- sweep_cell).
+// One more exact skip: phi_c always equals d(c, label_c) and only decreases, so once c
+// has examined label L, d(c, L) >= phi_c for ever after.  An interior cell examined
+// neighbour u in the last earlier sweep s' whose direction makes u upwind of c (seen[q]);
+// if u's label has not changed since (lc[u] <= s'+1), c has already seen that label.
+// With LIVE labels (the repair pass) this applies only while u still holds its
+// pre-sweep label, whose change history lc describes.
+template <bool LIVE>
+__device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
+                                                      int k, size_t c, unsigned long long own)
+{
+    const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
+    const long long cc = (long long)c;
+    const long long nb[7] = {cc - si, cc - sj, cc - si - sj, cc - sk, cc - si - sk, cc - sj - sk, cc - si - sj - sk};
+    int lab[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) lab[q] = (int)(uint32_t)(LIVE ? sp_ld64(L + nb[q]) : L[nb[q]]);
+    float phi = __uint_as_float((uint32_t)(own >> 32));
+    int ct = (int)(uint32_t)own;
+    const int ct0 = ct;
+    const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
+    const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const int t = lab[q];
+        bool skip = (t < 0) || (t == ct0);
+#pragma unroll
+        for (int r = 0; r < q; ++r) skip = skip || (lab[r] == t);
+        if (!skip && interior && P.seen[q] >= 0) {
+            const bool pre = LIVE ? (int)(uint32_t)P.S[nb[q]] == t : true;
+            if (pre && (int)P.lc[nb[q]] <= P.seen[q]) skip = true;
+        }
+        if (!skip) {
+            const float4 v0 = P.soup[3 * (size_t)t], v1 = P.soup[3 * (size_t)t + 1], v2 = P.soup[3 * (size_t)t + 2];
+            const float d = ptd(gx, mk3(v0.x, v0.y, v0.z), mk3(v1.x, v1.y, v1.z), mk3(v2.x, v2.y, v2.z));
+            if (d < phi) {
+                phi = d;
+                ct = t;
+            }
+        }
+    }
+    return ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
+}
+
+__device__ __forceinline__ void sp_enqueue(const SpParams &P, size_t e)
+{
+    atomicAdd(&P.ctl[SP_PENDING], 1ull);
+    const unsigned long long t = atomicAdd(&P.ctl[SP_TAIL], 1ull);
+    sp_st32(P.queue + t % P.cap, (unsigned)(e + 1));
+}
+
+// Request rechecks of the downstream neighbours of (i,j,k) (the cells whose upwind set
+// contains it).  Returns the first cell this call took ownership of when `claim`, so
+// the caller can run it itself; the others are queued.
+__device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i, int j, int k, size_t c, bool claim)
+{
+    const bool ii = P.di > 0 ? i + 1 <= P.ni - 1 : i - 1 >= 0;
+    const bool jj = P.dj > 0 ? j + 1 <= P.nj - 1 : j - 1 >= 0;
+    const bool kk = P.dk > 0 ? k + 1 <= P.nk - 1 : k - 1 >= 0;
+    const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
+    const long long cc = (long long)c;
+    // all requests in flight at once, then one reservation for the cells to queue
+    size_t tgt[7];
+    unsigned old[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        // same order as the upwind list: (i), (j), (i,j), (k), (i,k), (j,k), (i,j,k)
+        const int m = q + 1;
+        const bool ui = m & 1, uj = m & 2, uk = m & 4;
+        const bool ok = !((ui && !ii) || (uj && !jj) || (uk && !kk));
+        tgt[q] = ok ? (size_t)(cc + (ui ? si : 0) + (uj ? sj : 0) + (uk ? sk : 0)) : ~(size_t)0;
+        old[q] = ok ? atomicAdd(&P.req[tgt[q]], 1u) : 1u;
+    }
+    size_t mine = ~(size_t)0;
+    unsigned nq = 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        if (old[q] != 0u) continue;
+        if (claim && mine == ~(size_t)0) mine = tgt[q];
+        else ++nq;
+    }
+    if (nq) {
+        atomicAdd(&P.ctl[SP_PENDING], (unsigned long long)nq);
+        unsigned long long t = atomicAdd(&P.ctl[SP_TAIL], (unsigned long long)nq);
+#pragma unroll
+        for (int q = 0; q < 7; ++q)
+            if (old[q] == 0u && tgt[q] != mine) sp_st32(P.queue + (t++) % P.cap, (unsigned)(tgt[q] + 1));
+    }
+    return mine;
+}
+
+// Pass 1 of the sparse sweep: every cell against the labels of S.
+__global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
+{
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long c = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; c < P.n; c += stride) {
+        const unsigned c32 = (unsigned)c;   // n < 2^32 (sparse_sweep_supported)
+        const int i = (int)(c32 % (unsigned)P.ni);
+        const unsigned r = c32 / (unsigned)P.ni;
+        const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
+        const unsigned long long s = P.S[c];
+        if (!sp_in(P, i, j, k)) {
+            P.X[c] = s;
+            continue;
+        }
+        const unsigned long long y = sp_eval<false>(P, P.S, i, j, k, c, s);
+        P.X[c] = y;
+        if ((uint32_t)y != (uint32_t)s) {
+            P.lc[c] = (unsigned char)(P.sweep + 1);
+            sp_request_downstream(P, i, j, k, c, false);
+        }
+    }
+}
+
+// Pass 2: drain the recheck work list.  One lane = one worker; chains are followed
+// depth-first by the lane that changed the upstream cell.  Written as a flat loop in
+// which every lane does at most one poll or one evaluation per iteration: a lane
+// spinning on an empty slot must never hold back (SIMT reconvergence) lanes of its own
+// wave whose work would fill that slot.
+__global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
+{
+    constexpr size_t NONE = ~(size_t)0;
+    unsigned long long runs = 0, claims = 0, h = 0;
+    size_t e = NONE, next = NONE;
+    unsigned rq = 1;
+    bool done = false, waiting = false;
+    unsigned spins = 0;
+    for (;;) {
+        if (!done && e == NONE) {
+            if (!waiting) {
+                h = atomicAdd(&P.ctl[SP_HEAD], 1ull);
+                waiting = true;
+            }
+            unsigned *slot = P.queue + h % P.cap;
+            const unsigned v = sp_ld32(slot);
+            if (v) {
+                sp_st32(slot, 0u);
+                e = v - 1;
+                next = NONE;
+                rq = 1;
+                waiting = false;
+                spins = 0;
+            } else if (sp_ld64(&P.ctl[SP_PENDING]) == 0ull) {
+                done = true;   // nothing queued or running anywhere: no slot can fill any more
+            } else if (++spins > SP_WATCHDOG) {
+                atomicOr(&P.ctl[SP_ERR], 1ull);
+                done = true;
+            }
+        }
+        if (e != NONE) {
+            // one evaluation of cell e, retiring `rq` requests
+            const int i = (int)((unsigned)e % (unsigned)P.ni);
+            const unsigned r0 = (unsigned)e / (unsigned)P.ni;
+            const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
+            const unsigned long long cur = sp_ld64(P.X + e);
+            const unsigned long long y = sp_eval<true>(P, P.X, i, j, k, e, P.S[e]);
+            ++runs;
+            if (y != cur) {
+                sp_st64(P.X + e, y);
+                if ((uint32_t)y != (uint32_t)cur) {
+                    P.lc[e] = (unsigned char)(P.sweep + 1);
+                    sp_order();   // the new label is visible before anyone is asked to read it
+                    const size_t m = sp_request_downstream(P, i, j, k, e, next == NONE);
+                    if (m != NONE) next = m;
+                }
+            }
+            const unsigned old = atomicSub(P.req + e, rq);
+            if (old == rq) {   // no request arrived meanwhile: e is settled
+                if (next != NONE) {
+                    e = next;   // the work item's pending count carries over to the claimed cell
+                    next = NONE;
+                    rq = 1;
+                    ++claims;
+                } else {
+                    e = NONE;
+                    sp_order();
+                    atomicSub(&P.ctl[SP_PENDING], 1ull);
+                }
+            } else {
+                rq = old - rq;   // evaluate again for the requests that arrived meanwhile
+                sp_order();
+            }
+        }
+        if (__all(done)) break;
+        if (!__any(e != NONE)) __builtin_amdgcn_s_sleep(2);
+    }
+    if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
+    if (claims) atomicAdd(&P.ctl[SP_ENQ], claims);
+}
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct SparseSweepWorkspace {
+    int workers = SP_WORKERS_DEFAULT;            // repair-kernel workgroups (diagnostics may lower it)
+    unsigned long long *alt = nullptr;   // the second state buffer
+    unsigned *req = nullptr, *queue = nullptr;
+    unsigned long long *ctl = nullptr;
+    size_t cap_alt = 0, cap_req = 0, cap_queue = 0;
+};
+
+inline bool sparse_sweep_supported(unsigned long long n, int ni, int nj, int nk)
+{
+    return ni >= 2 && nj >= 2 && nk >= 2 && n + SP_WORKERS * 64ull + 1024ull < 0xffffffffull;
+}
+
+template <class T>
+inline int sp_grow(T **p, size_t *cap, size_t need, bool zero)
+{
+    if (*p && *cap >= need) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void **)p, need * sizeof(T)) != hipSuccess) return -5;
+    if (zero && hipMemset(*p, 0, need * sizeof(T)) != hipSuccess) return -4;
+    *cap = need;
+    return 0;
+}
+
+// Enqueue one sparse sweep on `st`: reads *cell, writes the other buffer, then swaps
+// the two so *cell holds the result.  Returns 0 or a negative SDFGEN_HIP_E* code.
+inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long **cell,
+                        size_t *cap_cell, unsigned char *lc, const float origin[3], float dx, int ni, int nj, int nk,
+                        int sweep)
+{
+    const int di = SP_DIRS[sweep % 8][0], dj = SP_DIRS[sweep % 8][1], dk = SP_DIRS[sweep % 8][2];
+    const unsigned long long n = (unsigned long long)ni * nj * nk;
+    const int nw = (W.workers > 0 && W.workers <= SP_WORKERS) ? W.workers : SP_WORKERS;
+    const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
+    if (sp_grow(&W.alt, &W.cap_alt, n, false)) return -5;
+    if (sp_grow(&W.req, &W.cap_req, n, true)) return -5;      // stays all-zero between sweeps
+    if (sp_grow(&W.queue, &W.cap_queue, cap, true)) return -5; // slots are reset when consumed
+    if (!W.ctl) {
+        if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
+        if (hipMemset(W.ctl, 0, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -4;
+    }
+    // per sweep: reset the list counters; error bits and statistics accumulate over the call
+    if (hipMemsetAsync(W.ctl, 0, 3 * sizeof(unsigned long long), st) != hipSuccess) return -4;
+    SpParams P;
+    P.soup = soup;
+    P.S = *cell;
+    P.X = W.alt;
+    P.req = W.req;
+    P.queue = W.queue;
+    P.ctl = W.ctl;
+    P.cap = cap;
+    P.n = n;
+    P.ox = origin[0];
+    P.oy = origin[1];
+    P.oz = origin[2];
+    P.dx = dx;
+    P.ni = ni;
+    P.nj = nj;
+    P.nk = nk;
+    P.di = di;
+    P.dj = dj;
+    P.dk = dk;
+    P.lc = lc;
+    P.sweep = sweep;
+    for (int q = 0; q < 7; ++q) {
+        const int m = q + 1;   // neighbour slot q lies upwind along the axes in mask m
+        P.seen[q] = -1;
+        for (int s2 = sweep - 1; s2 >= 0; --s2) {
+            const int *d = SP_DIRS[s2 % 8];
+            if ((!(m & 1) || d[0] == di) && (!(m & 2) || d[1] == dj) && (!(m & 4) || d[2] == dk)) {
+                P.seen[q] = s2 + 1;
+                break;
+            }
+        }
+    }
+    unsigned long long blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(k_sp_jacobi, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    if (hipGetLastError() != hipSuccess) return -4;
+    hipLaunchKernelGGL(k_sp_recheck, dim3(nw), dim3(64), 0, st, P);
+    if (hipGetLastError() != hipSuccess) return -4;
+    // swap the state buffers (both hold n cells)
+    unsigned long long *t = *cell;
+    const size_t tc = *cap_cell;
+    *cell = W.alt;
+    *cap_cell = W.cap_alt;
+    W.alt = t;
+    W.cap_alt = tc;
+    return 0;
+}
+
+inline void sparse_sweep_release(SparseSweepWorkspace &W)
+{
+    (void)hipFree(W.alt);
+    (void)hipFree(W.req);
+    (void)hipFree(W.queue);
+    (void)hipFree(W.ctl);
+    W = SparseSweepWorkspace();
+}
+
+}  // namespace sdfhip

@@ -1,5 +1,5 @@
 // sweep_tile.hpp -- one Gauss-Seidel sweep direction as ONE persistent launch:
-// a pipelined column wavefront over 8x8 (j,k) tiles, one compute wave per tile.
+// a pipelined column wavefront over 8x8 (j,k) tiles.
 //
 // Why this is exact.  The reference sweep (cpu_lib/makelevelset3.cpp:130-151)
 // visits k, then j, then i and updates each cell from its 7 upwind neighbours
@@ -9,25 +9,26 @@
 // neighbours first reproduces the sequential result bit-for-bit.
 //
 // Decomposition.  The (b,c) plane is cut into 8x8 tiles; a tile is one task for one
-// workgroup of two waves:
-//   * compute wave: lane (bl,cl) owns column (b0+bl, c0+cl) and at local step h
-//     updates cell a = h-bl-cl -- the whole tile advances one anti-diagonal per
-//     step with NO barrier: every intra-tile dependency is inside the wave, and a
-//     wave's LDS operations execute in order.  Neighbour results (label AND the
-//     triangle's vertices) live in an LDS ring, so no global load sits on the
-//     critical path.  The ~2 distinct candidates per cell (7 upwind labels minus
+// workgroup of ST_NCW compute waves and one helper wave:
+//   * compute waves: wave w owns the c-columns [w*CLW, (w+1)*CLW) of the tile; lane
+//     (bl,cl) owns column (b0+bl, c0+cl) and at local step h updates cell
+//     a = h-bl-cl.  A wave advances one anti-diagonal per step with no barrier:
+//     wave w starts step h once wave w-1 has finished step h-1 and while wave w+1 is
+//     at most RR-4 steps behind (LDS progress counters).  Neighbour results (label
+//     AND the triangle's vertices) live in an LDS ring, so no global load sits on
+//     the critical path.  The ~2 distinct candidates per cell (7 upwind labels minus
 //     duplicates and the cell's own label -- exact skips, see sweep_cell in
 //     sdfgen_hip.hip) are compacted across the wave (ballot + mbcnt) and evaluated
-//     two per lane with the branch-free ptd_nb, then each cell applies them in the
-//     reference's check order (strict '<', first minimum wins).
+//     one or two per lane with the branch-free ptd_nb, then each cell applies them
+//     in the reference's check order (strict '<', first minimum wins).
 //   * helper wave: batched, decoupled prefetch.  It streams each column's old
 //     (phi, label) and the label's vertices into an LDS "own" ring, and fills the
 //     17 halo streams (last row of tile J-1, last column of tile K-1, corner) from
 //     8-byte tagged granules {epoch, label} that producer tiles publish with one
 //     sc1 store each (the data is the flag: cdna_hip_programming.md G16 R2) plus a
 //     gather of the triangle's vertices from the read-only soup.  Readiness and
-//     ring capacity are LDS counters; the helper waits on global memory, the
-//     compute wave never does.
+//     ring capacity are LDS counters (capacity follows the SLOWEST compute wave);
+//     the helper waits on global memory, the compute waves never do.
 // Tasks are dequeued in anti-diagonal order (J+K, then J) from an atomic counter,
 // so every producer tile is claimed by a running workgroup before its consumers:
 // no residency assumption and no deadlock.  Every spin is bounded (watchdog).
@@ -37,28 +38,49 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <stdlib.h>
+
 #include <vector>
 
 #include "geom.hpp"
 
 namespace sdfhip {
 
-constexpr int ST_T = 8;                       // tile edge (b and c)
-constexpr int ST_NCOL = ST_T * ST_T;          // 64 columns = one wave
-constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edge (8), corner
-constexpr int ST_RO = 8;                      // own ring slots (steps)
-constexpr int ST_G = 4;                       // helper batch (steps / entries)
-#ifndef ST_RH_DEF
-#define ST_RH_DEF 32
-#endif
+// Tunables (compile-time; -D overrides are for experiments).  Defaults were chosen on
+// MI355X at 256^3: 3-wave workgroups with ~47 KB LDS let 3 tiles share
+// a CU, and that beat 5-wave / 79 KB tiles (1 per CU) by 12-15 %.
 #ifndef ST_NCW_DEF
-#define ST_NCW_DEF 4
+#define ST_NCW_DEF 2   // compute waves per tile
 #endif
-constexpr int ST_RH = ST_RH_DEF;                     // halo ring slots per stream (lead = RH-3 steps)
-constexpr int ST_NCW = ST_NCW_DEF;                     // compute waves per tile
-constexpr int ST_CLW = ST_T / ST_NCW;         // c-columns per compute wave (2)
-constexpr int ST_CPW = ST_T * ST_CLW;         // cells per compute wave (16)
-constexpr int ST_RR = 8;                      // neighbour ring slots (steps)
+#ifndef ST_RR_DEF
+#define ST_RR_DEF 8    // neighbour ring slots (power of two); lead between compute waves = RR-4
+#endif
+#ifndef ST_RO_DEF
+#define ST_RO_DEF 4    // own-column prefetch slots (power of two)
+#endif
+#ifndef ST_RH_DEF
+#define ST_RH_DEF 8    // halo ring slots per stream (power of two)
+#endif
+#ifndef ST_G_DEF
+#define ST_G_DEF 2     // helper batch: steps / halo entries per global round trip (2 or 4)
+#endif
+#ifndef ST_WPE_DEF
+#define ST_WPE_DEF 3   // waves per SIMD the register budget must allow
+#endif
+constexpr int ST_T = 8;                       // tile edge (b and c)
+constexpr int ST_NCOL = ST_T * ST_T;          // 64 columns
+constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edge (8), corner
+constexpr int ST_NCW = ST_NCW_DEF;
+constexpr int ST_CLW = ST_T / ST_NCW;         // c-columns per compute wave
+constexpr int ST_CPW = ST_T * ST_CLW;         // cells per compute wave
+constexpr int ST_RR = ST_RR_DEF;
+constexpr int ST_RO = ST_RO_DEF;
+constexpr int ST_RH = ST_RH_DEF;
+constexpr int ST_G = ST_G_DEF;
+static_assert(ST_NCW >= 1 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
+static_assert((ST_RR & (ST_RR - 1)) == 0 && ST_RR >= 4, "ring slots: power of two >= 4");
+static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
+static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
 constexpr int ST_LEAD = ST_RR - 4;            // max lead of wave w over wave w+1 (ring hazard)
 constexpr int ST_THREADS = 64 * (ST_NCW + 1); // compute waves + helper wave
 constexpr int ST_RING0 = 0;                                   // RR slots x 64 columns
@@ -82,6 +104,8 @@ struct StParams {
     int A, B, C, nJ, nK, ntasks;
     int di, dj, dk;
     unsigned epoch;
+    unsigned char *lc;            // optional: last sweep (+1) in which each cell's label changed
+    int sweep;
     int lead;                     // max steps wave w may run ahead of wave w+1 (<= ST_LEAD)
 };
 
@@ -126,7 +150,7 @@ __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v
     }
 }
 
-__global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
+__global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams P)
 {
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
     __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
@@ -363,8 +387,11 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                     s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __int_as_float(ct));
                     s_ent[3 * slot + 1] = w1;
                     s_ent[3 * slot + 2] = make_float4(w2.x, w2.y, w2.z, ST_TAGF(1, col_id, a));
-                    if (win >= 0)
-                        P.cell[st_phys(P, a, b, c)] = ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
+                    if (win >= 0) {   // a winner always carries a new label (own label is never a candidate)
+                        const size_t ph = st_phys(P, a, b, c);
+                        P.cell[ph] = ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
+                        if (P.lc) P.lc[ph] = (unsigned char)(P.sweep + 1);
+                    }
                     const unsigned long long gran = ((unsigned long long)P.epoch << 32) | (uint32_t)ct;
                     if (bl == ST_T - 1 && J < P.nJ - 1)
                         __hip_atomic_store(P.hb + ((size_t)J * P.C + c) * P.A + a, gran, __ATOMIC_RELAXED,
@@ -424,7 +451,7 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
             int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
             unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
-            static_assert(ST_G == 4, "helper pipeline is written out for 4-element batches");
+            static_assert(ST_G == 4 || ST_G == 2, "helper pipeline is written out for 2- or 4-element batches");
             // unused load slots read this lane's own column start (spread, cached), never one hot address
             const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, 0, 0);
             unsigned idle = 0;
@@ -455,8 +482,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
     const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
                 ST_GATHER(0, c0, q0)
                 ST_GATHER(1, c1, q1)
+#if ST_G_DEF > 2
                 ST_GATHER(2, c2, q2)
                 ST_GATHER(3, c3, q3)
+#endif
                 // ---- stage 1: issue batch B ----
                 const int fB = fA + gA;
                 int gB = min(ST_G, min(nsteps - fB, prog + ST_RO - fB));
@@ -482,8 +511,13 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
                 unsigned long long n0, n1, n2, n3, m0, m1, m2, m3;
                 ST_ISSUE(0, n0, m0)
                 ST_ISSUE(1, n1, m1)
+#if ST_G_DEF > 2
                 ST_ISSUE(2, n2, m2)
                 ST_ISSUE(3, n3, m3)
+#else
+                n2 = n3 = ~0ull;
+                m2 = m3 = 0ull;
+#endif
                 // ---- land batch A in LDS, then publish readiness ----
 #define ST_LAND(g, cg, qg)                                                                             \
     if (ST_OWN_OK(g)) {                                                                                \
@@ -500,8 +534,10 @@ __global__ void __launch_bounds__(ST_THREADS) k_sweep_tile(StParams P)
     }
                 ST_LAND(0, c0, q0)
                 ST_LAND(1, c1, q1)
+#if ST_G_DEF > 2
                 ST_LAND(2, c2, q2)
                 ST_LAND(3, c3, q3)
+#endif
 #undef ST_OWN_OK
 #undef ST_GATHER
 #undef ST_ISSUE
@@ -576,7 +612,7 @@ inline int st_grow(unsigned long long **p, size_t *cap, size_t need)
 
 // Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
-                      const float origin[3], float dx, int ni, int nj, int nk, int di, int dj, int dk, char *err,
+                      unsigned char *lc, const float origin[3], float dx, int ni, int nj, int nk, int di, int dj, int dk, char *err,
                       size_t errlen)
 {
     const int A = ni - 1, B = nj - 1, C = nk - 1;
@@ -644,9 +680,19 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.dj = dj;
     P.dk = dk;
     P.epoch = W.epoch;
+    P.lc = lc;
+    P.sweep = W.cur_sweep;
     P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
+    if (getenv("SDFGEN_OCC")) {   // diagnostics: resident workgroups per CU
+        int occ = -1;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sweep_tile, ST_THREADS, 0);
+        hipFuncAttributes fa;
+        (void)hipFuncGetAttributes(&fa, (const void *)k_sweep_tile);
+        fprintf(stderr, "k_sweep_tile: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", occ, fa.numRegs,
+                fa.sharedSizeBytes, fa.localSizeBytes);
+    }
     hipLaunchKernelGGL(k_sweep_tile, dim3(grid), dim3(ST_THREADS), 0, st, P);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;

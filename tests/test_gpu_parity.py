@@ -186,12 +186,20 @@ def test_gpu_device_entry_with_device_buffers():
 
 
 # ---------------------------------------------------------------- both sweep implementations
-@pytest.fixture(params=["plane", "wavefront"])
+# plane: one launch per hyperplane; tile: the column wavefront for all 16 sweeps;
+# hybrid (default): wavefront for the first pass, Jacobi + repair for the second;
+# sparse: Jacobi + repair for all 16 (stresses the repair protocol: most labels change).
+SWEEP_MODES = {"plane": ({"SDFGEN_SWEEP": "plane"}, 0), "tile": ({"SDFGEN_SPARSE_FROM": "16"}, 1),
+               "hybrid": ({}, 2), "sparse": ({"SDFGEN_SPARSE_FROM": "0"}, 2)}
+
+
+@pytest.fixture(params=list(SWEEP_MODES))
 def sweep_impl(request, monkeypatch):
-    if request.param == "plane":
-        monkeypatch.setenv("SDFGEN_SWEEP", "plane")
-    else:
-        monkeypatch.delenv("SDFGEN_SWEEP", raising=False)
+    for k in ("SDFGEN_SWEEP", "SDFGEN_SPARSE_FROM"):
+        monkeypatch.delenv(k, raising=False)
+    env, _ = SWEEP_MODES[request.param]
+    for k, val in env.items():
+        monkeypatch.setenv(k, val)
     return request.param
 
 
@@ -210,5 +218,8 @@ def test_gpu_sweep_impls_agree_with_oracle(sweep_impl, nu, nv, dims):
     o, dx = meshgen.grid_mode2b(v, *dims, 2)
     want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, *dims, exact_band=1))
     got = _lib.make_level_set3(v, t, o, dx, *dims, 1)
-    assert _lib.last_profile()["sweep_impl"] == (0 if sweep_impl == "plane" else 1)
+    prof = _lib.last_profile()
+    assert prof["sweep_impl"] == SWEEP_MODES[sweep_impl][1]
+    if sweep_impl == "sparse":
+        assert prof["sparse_sweeps"] == 16 and prof["sparse_rechecks"] > 0
     assert bits_equal(got, want), diff_report(got, want, dx)
