@@ -111,15 +111,28 @@ def main():
 
     ms_step = el / args.steps * 1e3
     value = world * ncell * args.steps / el / 1e6
-    # dominant kernel: the sweep.  Per-launch duration from the library's HIP events on the launch stream.
-    sweep_ms = sum(p["sweep_ms"] for p in profs) / len(profs)
-    launches = profs[-1]["sweep_launches"]
+    # Dominant kernel: the tile-wavefront sweep (k_sweep_tile), one launch per first-pass
+    # sweep.  Its per-launch duration is the library's HIP-event time around that launch on
+    # the launch stream; algorithmic bytes per launch = 16 B per swept cell.
+    last = profs[-1]
+    n_tile = last["sparse_first"] if last["sparse_sweeps"] else 16
     A, B, C = ni - 1, nj - 1, nk - 1
-    bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * C * 16 / max(launches, 1)
-    launch_ms = sweep_ms / max(launches, 1)
+    tile_ms = [sum(p["sweep_launch_ms"][s] for p in profs) / len(profs) for s in range(n_tile)]
+    launch_ms = sum(tile_ms) / max(len(tile_ms), 1)
+    bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * C
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
+    sparse_ms = [sum(p["sweep_launch_ms"][s] for p in profs) / len(profs) for s in range(n_tile, 16)]
     phases = {k: round(sum(p[k] for p in profs) / len(profs), 4)
               for k in ("prep_ms", "band_ms", "sweep_ms", "sign_ms", "total_ms")}
+    phases["tile_sweeps_ms"] = round(sum(tile_ms), 4)
+    phases["sparse_sweeps_ms"] = round(sum(sparse_ms), 4)
+    traffic, traffic_src = None, None
+    tp = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if os.path.exists(tp):
+        rec = json.load(open(tp))
+        k = rec.get("kernels", {}).get("k_sweep_tile")
+        if rec.get("workload") == args.workload and k:
+            traffic, traffic_src = k["hbm_bytes_per_launch"], "profiles/pmc_summary.json"
 
     parity = None
     if not args.no_verify and rank == 0:
@@ -149,9 +162,9 @@ def main():
                        "exact_band": 1, "parallelism": "replicas" if world > 1 else "single-gpu",
                        "inputs": "HBM-resident"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": "sweep", "launches_per_step": launches,
-                         "avg_launch_ms": round(launch_ms, 5),
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         "traffic_source": traffic_src, "kernel": "k_sweep_tile",
+                         "launches_per_step": n_tile, "avg_launch_ms": round(launch_ms, 5),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch)},
             "phases_ms": phases,
             "sweep_impl": profs[-1]["sweep_impl"],

@@ -96,7 +96,8 @@ typedef struct sdfgen_hip_profile {
     double sweep_launch_ms[16];  /* per (pass, direction) sweep */
     int sweep_launches;       /* kernel launches issued for the sweeps */
     int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined 8x8-tile column wavefront,
-                                 2 = tile wavefront for the first pass + Jacobi/repair for sparse sweeps */
+                                 2 = tile wavefront for the first pass + Jacobi/repair for sparse sweeps,
+                                 3 = Z-slab tile wavefront (sdfgen_hip_slab_*) */
     uint64_t band_evals;      /* point-triangle evaluations in the band phase */
     uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless SDFGEN_COUNT_EVALS is set) */
     uint64_t sweep_stalls;    /* compute-wave polls that found a hand-off not yet landed (same) */
@@ -112,6 +113,48 @@ int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
 
 /* Free cached device workspaces (they are grow-only between calls). */
 int sdfgen_hip_release(void);
+
+/* ---------------------------------------------------------------------------
+ * Z-slab decomposition over several GPUs (north_star: "the voxel grid shards along Z
+ * into per-GPU slabs").  No reference counterpart -- the reference is single-device
+ * (README.md:220 lists multi-GPU as future work); SURVEY.md §8.e.
+ *
+ * A session owns planes k in [k_begin, k_end) of an ni x nj x nk grid (slab s of n:
+ * k_begin = s*nk/n).  Band, ray parity and sign are local.  Each of the 16 sweeps runs
+ * the tile wavefront on the slab; the boundary plane travels between neighbouring
+ * slabs as tagged granules written straight into the neighbour's inbox (xGMI, the
+ * inbox memory is mapped across processes with HIP IPC), so the wavefront pipelines
+ * across GPUs inside every sweep.  Result bits equal the single-GPU / reference bits.
+ *
+ * One process per GPU:   create -> export (IPC handle) -> exchange handles (e.g.
+ * torch.distributed all_gather) -> connect_ipc(lower, upper) -> barrier -> run.
+ * Several slabs in one process (any devices): create each -> connect_local.
+ * enqueue/finish split lets one thread drive several sessions concurrently. */
+typedef struct sdfgen_hip_slab sdfgen_hip_slab;
+#define SDFGEN_HIP_IPC_HANDLE_BYTES 64
+
+int sdfgen_hip_slab_create(int device, int nslabs, int slab, int ni, int nj, int nk, sdfgen_hip_slab **out,
+                           char *errbuf, size_t errlen);
+int sdfgen_hip_slab_range(const sdfgen_hip_slab *s, int *k_begin, int *k_end);
+/* handle: SDFGEN_HIP_IPC_HANDLE_BYTES bytes describing this slab's inboxes */
+int sdfgen_hip_slab_export(sdfgen_hip_slab *s, void *handle, char *errbuf, size_t errlen);
+/* lower/upper: the neighbours' exported handles (NULL for slab 0 / the last slab) */
+int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *s, const void *lower, const void *upper, char *errbuf,
+                                size_t errlen);
+int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *s, sdfgen_hip_slab *lower, sdfgen_hip_slab *upper,
+                                  char *errbuf, size_t errlen);
+/* Device buffers on the session's GPU; d_phi_slab receives ni*nj*(k_end-k_begin) floats in
+ * the chosen layout (ARRAY3: i fastest, the slab's planes only; KFAST: k fastest). */
+int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *s, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
+                            uint64_t nvert, const float origin[3], float dx, int exact_band, int out_layout,
+                            float *d_phi_slab, char *errbuf, size_t errlen);
+int sdfgen_hip_slab_finish(sdfgen_hip_slab *s, uint64_t nvert, sdfgen_hip_profile *prof, char *errbuf,
+                           size_t errlen);
+/* Host buffers: upload, enqueue, download into phi_slab, finish. */
+int sdfgen_hip_slab_run(sdfgen_hip_slab *s, const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert,
+                        const float origin[3], float dx, int exact_band, int out_layout, float *phi_slab,
+                        sdfgen_hip_profile *prof, char *errbuf, size_t errlen);
+int sdfgen_hip_slab_destroy(sdfgen_hip_slab *s);
 
 /* Diagnostics (used by the parity tests): evaluate the device geometry kernels
  * on host arrays.  pts: n x 12 floats (x0,x1,x2,x3) -> out: n floats;

@@ -34,7 +34,17 @@ EXPORTED = (
     "sdfgen_hip_debug_pit2d",
     "sdfgen_cpu_make_level_set3",
     "sdfgen_hip_debug_sweep_trace",
+    "sdfgen_hip_slab_create",
+    "sdfgen_hip_slab_range",
+    "sdfgen_hip_slab_export",
+    "sdfgen_hip_slab_connect_ipc",
+    "sdfgen_hip_slab_connect_local",
+    "sdfgen_hip_slab_enqueue",
+    "sdfgen_hip_slab_finish",
+    "sdfgen_hip_slab_run",
+    "sdfgen_hip_slab_destroy",
 )
+IPC_HANDLE_BYTES = 64
 
 
 class Profile(ctypes.Structure):
@@ -93,6 +103,20 @@ def _load():
     L.sdfgen_hip_debug_pit2d.restype = ctypes.c_int
     L.sdfgen_hip_debug_sweep_trace.argtypes = [ctypes.c_int, _P, _u64, ctypes.POINTER(_u64)]
     L.sdfgen_hip_debug_sweep_trace.restype = ctypes.c_int
+    _E = [ctypes.c_char_p, ctypes.c_size_t]
+    L.sdfgen_hip_slab_create.argtypes = [ctypes.c_int] * 6 + [ctypes.POINTER(_P)] + _E
+    L.sdfgen_hip_slab_range.argtypes = [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.sdfgen_hip_slab_export.argtypes = [_P, _P] + _E
+    L.sdfgen_hip_slab_connect_ipc.argtypes = [_P, _P, _P] + _E
+    L.sdfgen_hip_slab_connect_local.argtypes = [_P, _P, _P] + _E
+    L.sdfgen_hip_slab_enqueue.argtypes = [_P, _P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                          _P] + _E
+    L.sdfgen_hip_slab_finish.argtypes = [_P, _u64, ctypes.POINTER(Profile)] + _E
+    L.sdfgen_hip_slab_run.argtypes = [_P, _P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int, _P,
+                                      ctypes.POINTER(Profile)] + _E
+    L.sdfgen_hip_slab_destroy.argtypes = [_P]
+    for f in ("create", "range", "export", "connect_ipc", "connect_local", "enqueue", "finish", "run", "destroy"):
+        getattr(L, "sdfgen_hip_slab_" + f).restype = ctypes.c_int
     return L
 
 
@@ -213,3 +237,85 @@ def debug_pit2d(pit: np.ndarray, device: int = 0) -> np.ndarray:
     if rc != OK:
         _raise(rc, err)
     return out
+
+
+class Slab:
+    """One Z-slab session (sdfgen_hip_slab_*): planes k in [k_begin, k_end) on `device`."""
+
+    def __init__(self, device: int, nslabs: int, slab: int, ni: int, nj: int, nk: int):
+        self.dims = (int(ni), int(nj), int(nk))
+        self.device, self.nslabs, self.slab = int(device), int(nslabs), int(slab)
+        h = _P()
+        err = ctypes.create_string_buffer(512)
+        rc = lib.sdfgen_hip_slab_create(self.device, self.nslabs, self.slab, *self.dims, ctypes.byref(h), err,
+                                        ctypes.sizeof(err))
+        if rc != OK:
+            _raise(rc, err)
+        self.h = h
+        kb, ke = ctypes.c_int(), ctypes.c_int()
+        lib.sdfgen_hip_slab_range(self.h, ctypes.byref(kb), ctypes.byref(ke))
+        self.k_begin, self.k_end = kb.value, ke.value
+
+    def _check(self, rc, err):
+        if rc != OK:
+            _raise(rc, err)
+
+    def export(self) -> bytes:
+        buf = ctypes.create_string_buffer(IPC_HANDLE_BYTES)
+        err = ctypes.create_string_buffer(512)
+        self._check(lib.sdfgen_hip_slab_export(self.h, buf, err, ctypes.sizeof(err)), err)
+        return buf.raw
+
+    def connect_ipc(self, lower: bytes | None, upper: bytes | None) -> None:
+        err = ctypes.create_string_buffer(512)
+        lo = ctypes.create_string_buffer(lower, IPC_HANDLE_BYTES) if lower else None
+        up = ctypes.create_string_buffer(upper, IPC_HANDLE_BYTES) if upper else None
+        self._check(lib.sdfgen_hip_slab_connect_ipc(self.h, lo, up, err, ctypes.sizeof(err)), err)
+
+    def connect_local(self, lower: "Slab | None", upper: "Slab | None") -> None:
+        err = ctypes.create_string_buffer(512)
+        self._check(lib.sdfgen_hip_slab_connect_local(self.h, lower.h if lower else None, upper.h if upper else None,
+                                                      err, ctypes.sizeof(err)), err)
+
+    def enqueue(self, d_tri: int, ntri: int, d_xyz: int, nvert: int, origin, dx: float, exact_band: int,
+                layout: int, d_out: int) -> None:
+        o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+        err = ctypes.create_string_buffer(512)
+        self._check(lib.sdfgen_hip_slab_enqueue(self.h, _P(d_tri), int(ntri), _P(d_xyz), int(nvert),
+                                                o.ctypes.data_as(_P), ctypes.c_float(dx), int(exact_band),
+                                                int(layout), _P(d_out), err, ctypes.sizeof(err)), err)
+
+    def finish(self, nvert: int = 0) -> dict:
+        p = Profile()
+        err = ctypes.create_string_buffer(512)
+        self._check(lib.sdfgen_hip_slab_finish(self.h, int(nvert), ctypes.byref(p), err, ctypes.sizeof(err)), err)
+        return p.as_dict()
+
+    def run(self, vertices, triangles, origin, dx: float, exact_band: int = 1, layout: int = LAYOUT_ARRAY3):
+        """Host arrays in; returns (phi slab (ni,nj,k_end-k_begin) indexed [i,j,k-k_begin], profile)."""
+        v = np.ascontiguousarray(vertices, dtype=np.float32)
+        t = np.ascontiguousarray(triangles, dtype=np.uint32)
+        o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+        ni, nj, _ = self.dims
+        nks = self.k_end - self.k_begin
+        out = np.empty(ni * nj * nks, dtype=np.float32)
+        p = Profile()
+        err = ctypes.create_string_buffer(512)
+        self._check(lib.sdfgen_hip_slab_run(self.h, t.ctypes.data_as(_P), t.size // 3, v.ctypes.data_as(_P),
+                                            v.size // 3, o.ctypes.data_as(_P), ctypes.c_float(dx), int(exact_band),
+                                            int(layout), out.ctypes.data_as(_P), ctypes.byref(p), err,
+                                            ctypes.sizeof(err)), err)
+        if layout == LAYOUT_KFAST:
+            return out.reshape((ni, nj, nks)), p.as_dict()
+        return out.reshape((ni, nj, nks), order="F"), p.as_dict()
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib.sdfgen_hip_slab_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -111,9 +111,12 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 
 // Narrow band + ray parity, one 64-lane wave per triangle (grid-stride over triangles).
 //   :206-220 band, :222-235 parity
+// [k_lo, k_hi): the k planes this call owns (a Z-slab; 0..nk for the whole grid).  Boxes are
+// clamped to the whole grid first (:210-212), then cut to the slab, so every slab sees
+// exactly the reference's cells.
 __global__ void __launch_bounds__(256) k_band(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
                                               float init, u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
-                                              unsigned long long *__restrict__ eval_count)
+                                              unsigned long long *__restrict__ eval_count, int k_lo, int k_hi)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
@@ -131,6 +134,8 @@ __global__ void __launch_bounds__(256) k_band(const float4 *__restrict__ soup, u
         int j1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fjp, fjq, fjr)), band), 1), 0, g.nj - 1);
         int k0 = clampi(wrap_add(trunc_to_int(dmin3(fkp, fkq, fkr)), -band), 0, g.nk - 1);
         int k1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fkp, fkq, fkr)), band), 1), 0, g.nk - 1);
+        k0 = max(k0, k_lo);
+        k1 = min(k1, k_hi - 1);
         if (i1 >= i0 && j1 >= j0 && k1 >= k0) {
             const uint32_t bi = (uint32_t)(i1 - i0 + 1), bj = (uint32_t)(j1 - j0 + 1);
             const uint64_t bij = (uint64_t)bi * bj;
@@ -155,6 +160,8 @@ __global__ void __launch_bounds__(256) k_band(const float4 *__restrict__ soup, u
         int pj1 = clampi(trunc_to_int(floor(dmax3(fjp, fjq, fjr))), 0, g.nj - 1);
         int pk0 = clampi(trunc_to_int(ceil(dmin3(fkp, fkq, fkr))), 0, g.nk - 1);
         int pk1 = clampi(trunc_to_int(floor(dmax3(fkp, fkq, fkr))), 0, g.nk - 1);
+        pk0 = max(pk0, k_lo);
+        pk1 = min(pk1, k_hi - 1);
         if (pj1 >= pj0 && pk1 >= pk0) {
             const uint32_t bj = (uint32_t)(pj1 - pj0 + 1);
             const uint64_t total = (uint64_t)bj * (uint64_t)(pk1 - pk0 + 1);
@@ -235,14 +242,15 @@ __global__ void __launch_bounds__(256) k_sweep_plane(const float4 *__restrict__ 
 
 // Sign pass: one wave per (j,k) row; prefix parity by ballot, sign flip (-0.0 kept),
 // output in Array3f (i-fastest) or k-fastest layout.   :294-303
+// Rows k in [k_lo, k_lo + k_cnt); the output holds just those planes.
 __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, const uint32_t *__restrict__ cnt, Grid g,
-                                              int layout, float *__restrict__ out)
+                                              int layout, float *__restrict__ out, int k_lo, int k_cnt)
 {
     const int lane = threadIdx.x & 63;
     const uint64_t row = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nrows = (uint64_t)g.nj * g.nk;
+    const uint64_t nrows = (uint64_t)g.nj * k_cnt;
     if (row >= nrows) return;
-    const int j = (int)(row % g.nj), k = (int)(row / g.nj);
+    const int j = (int)(row % g.nj), k = k_lo + (int)(row / g.nj);
     const size_t base = cidx(0, j, k, g.ni, g.nj);
     uint32_t carry = 0;
     for (int i0 = 0; i0 < g.ni; i0 += 64) {
@@ -256,8 +264,8 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
             uint32_t bits = (uint32_t)(cell[base + i] >> 32);
             if (pre) bits ^= 0x80000000u;
             float v = __uint_as_float(bits);
-            if (layout == SDFGEN_LAYOUT_ARRAY3) out[base + i] = v;
-            else out[((size_t)i * g.nj + j) * g.nk + k] = v;
+            if (layout == SDFGEN_LAYOUT_ARRAY3) out[cidx(i, j, k - k_lo, g.ni, g.nj)] = v;
+            else out[((size_t)i * g.nj + j) * k_cnt + (k - k_lo)] = v;
         }
         carry = (carry + (uint32_t)__popcll(mask)) & 1u;
     }
@@ -405,7 +413,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipEventRecord(ev[1], st));
     if (ntri) {
         hipLaunchKernelGGL(k_band, dim3(grid_for(ntri * 64, 256, 65536)), dim3(256), 0, st, ws->soup, ntri, g, band,
-                           init, ws->cell, ws->cnt, ws->evals);
+                           init, ws->cell, ws->cnt, ws->evals, 0, nk);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[2], st));
@@ -484,7 +492,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     {
         const uint64_t rows = (uint64_t)nj * nk;
         hipLaunchKernelGGL(k_sign, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, st, ws->cell, ws->cnt, g,
-                           layout, d_out);
+                           layout, d_out, 0, nk);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[20], st));
@@ -546,6 +554,216 @@ int device_count_impl()
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+
+// ---------------------------------------------------------------------------
+// Z-slab sessions: one slab of k planes per GPU (one process per GPU, or several
+// slabs in one process).  DESIGN.md §7.
+//   * band, ray parity, sign: local to the slab (boxes clamped to the whole grid first);
+//   * each sweep: the tile wavefront runs over this slab's oriented c range; the plane
+//     just upstream arrives as tagged granules in an inbox written by the upstream GPU
+//     (over xGMI, IPC-mapped), and this slab's last plane is written into the
+//     downstream GPU's inbox -- the wavefront pipelines straight across GPUs.
+//   * inboxes alternate by sweep parity: consecutive sweeps in the same k direction
+//     (3,4 / 1,2 / ...) never share a buffer, and a producer cannot start the sweep
+//     after next before its consumer finished reading (it needs that consumer's
+//     granules in between).
+// ---------------------------------------------------------------------------
+struct SlabSession {
+    int device = -1, nslabs = 1, slab = 0, ni = 0, nj = 0, nk = 0, k_begin = 0, k_end = 0;
+    hipStream_t stream = nullptr;
+    u64 *cell = nullptr;
+    uint32_t *cnt = nullptr;
+    float4 *soup = nullptr;
+    uint32_t *tri = nullptr;
+    float *xyz = nullptr, *out = nullptr;
+    int *err_flag = nullptr;
+    unsigned long long *evals = nullptr;
+    size_t cap_soup = 0, cap_tri = 0, cap_xyz = 0, cap_out = 0;
+    TileSweepWorkspace wf;
+    u64 *inbox_mem = nullptr;   // 4 planes: [from lower (dk>0)][parity], [from upper (dk<0)][parity]
+    size_t plane = 0;           // granules per plane: (ni) x (nj)  -- a, b in [-1, A) x [-1, B)
+    u64 *peer_lower = nullptr, *peer_upper = nullptr;   // neighbours' inbox_mem (mapped)
+    bool lower_ipc = false, upper_ipc = false;
+    hipEvent_t ev[24] = {};
+    int launches = 0;
+    std::mutex mu;
+
+    u64 *inbox(int from_upper, int parity) const { return inbox_mem + plane * (2 * from_upper + parity); }
+};
+
+int slab_alloc(SlabSession *S, Err &err)
+{
+    HIPCHK(hipSetDevice(S->device));
+    HIPCHK(hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
+    for (auto &e : S->ev) HIPCHK(hipEventCreate(&e));
+    const uint64_t n = (uint64_t)S->ni * S->nj * S->nk;
+    HIPCHK(hipMalloc((void **)&S->cell, n * sizeof(u64)));
+    HIPCHK(hipMalloc((void **)&S->cnt, n * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void **)&S->err_flag, sizeof(int)));
+    HIPCHK(hipMalloc((void **)&S->evals, sizeof(unsigned long long)));
+    S->plane = (size_t)S->ni * S->nj;
+    HIPCHK(hipMalloc((void **)&S->inbox_mem, 4 * S->plane * sizeof(u64)));
+    HIPCHK(hipMemset(S->inbox_mem, 0, 4 * S->plane * sizeof(u64)));   // epoch 0 is never published
+    HIPCHK(hipDeviceSynchronize());
+    return 0;
+}
+
+void slab_free(SlabSession *S)
+{
+    if (S->device < 0) return;
+    (void)hipSetDevice(S->device);
+    if (S->stream) (void)hipStreamSynchronize(S->stream);
+    if (S->lower_ipc && S->peer_lower) (void)hipIpcCloseMemHandle(S->peer_lower);
+    if (S->upper_ipc && S->peer_upper) (void)hipIpcCloseMemHandle(S->peer_upper);
+    (void)hipFree(S->cell);
+    (void)hipFree(S->cnt);
+    (void)hipFree(S->soup);
+    (void)hipFree(S->tri);
+    (void)hipFree(S->xyz);
+    (void)hipFree(S->out);
+    (void)hipFree(S->err_flag);
+    (void)hipFree(S->evals);
+    (void)hipFree(S->inbox_mem);
+    tile_sweep_release(S->wf);
+    for (auto &e : S->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (S->stream) (void)hipStreamDestroy(S->stream);
+}
+
+// Oriented c range of this slab for a sweep with k direction dk (see sweep_tile.hpp).
+void slab_c_range(const SlabSession *S, int dk, int *cs, int *ce)
+{
+    if (dk > 0) {
+        *cs = std::max(S->k_begin, 1) - 1;
+        *ce = S->k_end - 1;
+    } else {
+        *cs = S->nk - 1 - std::min(S->k_end, S->nk - 1);
+        *ce = S->nk - 1 - S->k_begin;
+    }
+}
+
+// Enqueue the whole pipeline for this slab on S->stream (inputs/outputs on S->device).
+int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz, uint64_t nvert,
+                 const float origin[3], float dx, int band, int layout, float *d_out, Err &err)
+{
+    const int ni = S->ni, nj = S->nj, nk = S->nk;
+    const uint64_t plane_cells = (uint64_t)ni * nj;
+    const int kc = S->k_end - S->k_begin;
+    if (!S->soup || S->cap_soup < 3 * std::max<uint64_t>(ntri, 1)) {
+        if (S->soup) HIPCHK(hipFree(S->soup));
+        S->soup = nullptr;
+        S->cap_soup = 0;
+        HIPCHK(hipMalloc((void **)&S->soup, 3 * std::max<uint64_t>(ntri, 1) * sizeof(float4)));
+        S->cap_soup = 3 * std::max<uint64_t>(ntri, 1);
+    }
+    hipStream_t st = S->stream;
+    Grid g{origin[0], origin[1], origin[2], dx, ni, nj, nk};
+    const float init = (float)(ni + nj + nk) * dx;
+    const u64 init_key = ((u64)__builtin_bit_cast(uint32_t, init) << 32) | 0xffffffffull;
+    hipEvent_t *ev = S->ev;
+    HIPCHK(hipEventRecord(ev[0], st));
+    HIPCHK(hipMemsetAsync(S->err_flag, 0, sizeof(int), st));
+    HIPCHK(hipMemsetAsync(S->evals, 0, sizeof(unsigned long long), st));
+    if (S->wf.ctrl) HIPCHK(hipMemsetAsync(S->wf.ctrl + 1, 0, 2 * sizeof(int), st));
+    if (ntri) {
+        hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, d_tri, ntri, d_xyz, nvert,
+                           S->soup, S->err_flag);
+        HIPCHK(hipGetLastError());
+    }
+    const uint64_t nslab = plane_cells * kc;
+    hipLaunchKernelGGL(k_init, dim3(grid_for(nslab, 256, 8192)), dim3(256), 0, st, S->cell + plane_cells * S->k_begin,
+                       S->cnt + plane_cells * S->k_begin, nslab, init_key);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(ev[1], st));
+    if (ntri) {
+        hipLaunchKernelGGL(k_band, dim3(grid_for(ntri * 64, 256, 65536)), dim3(256), 0, st, S->soup, ntri, g, band,
+                           init, S->cell, S->cnt, S->evals, S->k_begin, S->k_end);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[2], st));
+    S->launches = 0;
+    const bool do_sweep = ni >= 2 && nj >= 2 && nk >= 2 && ntri > 0;
+    {
+        const char *gr = getenv("SDFGEN_TILE_GRID");   // co-resident slabs on one GPU need a cap
+        S->wf.grid_override = gr ? atoi(gr) : 0;
+    }
+    for (int s = 0; s < 16; ++s) {
+        HIPCHK(hipEventRecord(ev[3 + s], st));
+        if (!do_sweep) continue;
+        const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
+        TileSlab sl;
+        sl.on = true;
+        slab_c_range(S, dk, &sl.cs, &sl.ce);
+        const int par = s & 1;
+        if (dk > 0) {
+            sl.in = S->slab > 0 ? S->inbox(0, par) : nullptr;
+            sl.out = S->peer_upper ? S->peer_upper + S->plane * (0 + par) : nullptr;
+        } else {
+            sl.in = S->slab < S->nslabs - 1 ? S->inbox(1, par) : nullptr;
+            sl.out = S->peer_lower ? S->peer_lower + S->plane * (2 + par) : nullptr;
+        }
+        S->wf.cur_sweep = s;
+        int rc = tile_sweep(S->wf, st, S->soup, S->cell, nullptr, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
+                            err.len, sl);
+        if (rc) return rc;
+        ++S->launches;
+    }
+    HIPCHK(hipEventRecord(ev[19], st));
+    {
+        const uint64_t rows = (uint64_t)nj * kc;
+        hipLaunchKernelGGL(k_sign, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, st, S->cell, S->cnt, g,
+                           layout, d_out, S->k_begin, kc);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[20], st));
+    return 0;
+}
+
+int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &err)
+{
+    hipStream_t st = S->stream;
+    int flag = 0, wf_err[2] = {0, 0};
+    unsigned long long evals = 0;
+    HIPCHK(hipMemcpyAsync(&flag, S->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (S->wf.ctrl) HIPCHK(hipMemcpyAsync(wf_err, S->wf.ctrl + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&evals, S->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (prof) {
+        sdfgen_hip_profile p;
+        memset(&p, 0, sizeof(p));
+        float ms = 0;
+        hipEvent_t *ev = S->ev;
+        HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[20]));
+        p.total_ms = ms;
+        HIPCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
+        p.prep_ms = ms;
+        HIPCHK(hipEventElapsedTime(&ms, ev[1], ev[2]));
+        p.band_ms = ms;
+        HIPCHK(hipEventElapsedTime(&ms, ev[3], ev[19]));
+        p.sweep_ms = ms;
+        for (int s = 0; s < 16; ++s) {
+            HIPCHK(hipEventElapsedTime(&ms, ev[3 + s], ev[(s == 15) ? 19 : 4 + s]));
+            p.sweep_launch_ms[s] = ms;
+        }
+        HIPCHK(hipEventElapsedTime(&ms, ev[19], ev[20]));
+        p.sign_ms = ms;
+        p.sweep_launches = S->launches;
+        p.sweep_impl = 3;   // Z-slab tile wavefront
+        p.band_evals = evals;
+        p.sparse_first = 16;
+        *prof = p;
+    }
+    if (wf_err[0] & 4)
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: upstream slab's plane never arrived (sweep %d)", S->slab,
+                       wf_err[1] - 1);
+    if (wf_err[0])
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: sweep watchdog fired (lost tile hand-off, code %d, sweep %d)",
+                       S->slab, wf_err[0], wf_err[1] - 1);
+    if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
+                             (unsigned long long)nvert);
+    return 0;
 }
 
 }  // namespace
@@ -701,6 +919,183 @@ int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *ou
     HIPCHK(hipMemcpy(out4, dout, n * 4 * sizeof(double), hipMemcpyDeviceToHost));
     hipFree(dp);
     hipFree(dout);
+    return 0;
+}
+
+
+// ---------------------------------------------------------------- Z-slab sessions
+struct sdfgen_hip_slab {
+    SlabSession s;
+};
+
+int sdfgen_hip_slab_create(int device, int nslabs, int slab, int ni, int nj, int nk, sdfgen_hip_slab **out,
+                           char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    if (!out) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    *out = nullptr;
+    int rc = validate(0, 0, 1.0f, ni, nj, nk, SDFGEN_LAYOUT_ARRAY3, err);
+    if (rc) return rc;
+    if (nslabs < 1 || slab < 0 || slab >= nslabs) return err.set(SDFGEN_HIP_EINVAL, "slab %d of %d", slab, nslabs);
+    if (nk < 2 * nslabs) return err.set(SDFGEN_HIP_EINVAL, "nz = %d too small for %d slabs (need >= 2 planes each)", nk, nslabs);
+    if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "GPU device %d not available", device);
+    sdfgen_hip_slab *h = new sdfgen_hip_slab();
+    SlabSession *S = &h->s;
+    S->device = device;
+    S->nslabs = nslabs;
+    S->slab = slab;
+    S->ni = ni;
+    S->nj = nj;
+    S->nk = nk;
+    S->k_begin = (int)((long long)slab * nk / nslabs);
+    S->k_end = (int)((long long)(slab + 1) * nk / nslabs);
+    if ((rc = slab_alloc(S, err))) {
+        slab_free(S);
+        delete h;
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int sdfgen_hip_slab_range(const sdfgen_hip_slab *h, int *k_begin, int *k_end)
+{
+    if (!h || !k_begin || !k_end) return SDFGEN_HIP_EINVAL;
+    *k_begin = h->s.k_begin;
+    *k_end = h->s.k_end;
+    return 0;
+}
+
+int sdfgen_hip_slab_export(sdfgen_hip_slab *h, void *handle, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (!h || !handle) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    static_assert(sizeof(hipIpcMemHandle_t) <= SDFGEN_HIP_IPC_HANDLE_BYTES, "IPC handle size");
+    HIPCHK(hipSetDevice(h->s.device));
+    hipIpcMemHandle_t m;
+    HIPCHK(hipIpcGetMemHandle(&m, h->s.inbox_mem));
+    memset(handle, 0, SDFGEN_HIP_IPC_HANDLE_BYTES);
+    memcpy(handle, &m, sizeof(m));
+    return 0;
+}
+
+int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *h, const void *lower, const void *upper, char *errbuf,
+                                size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    SlabSession *S = &h->s;
+    if ((S->slab > 0) != (lower != nullptr) || (S->slab < S->nslabs - 1) != (upper != nullptr))
+        return err.set(SDFGEN_HIP_EINVAL, "slab %d of %d needs exactly its existing neighbours", S->slab, S->nslabs);
+    HIPCHK(hipSetDevice(S->device));
+    if (lower) {
+        hipIpcMemHandle_t m;
+        memcpy(&m, lower, sizeof(m));
+        void *p = nullptr;
+        HIPCHK(hipIpcOpenMemHandle(&p, m, hipIpcMemLazyEnablePeerAccess));
+        S->peer_lower = (u64 *)p;
+        S->lower_ipc = true;
+    }
+    if (upper) {
+        hipIpcMemHandle_t m;
+        memcpy(&m, upper, sizeof(m));
+        void *p = nullptr;
+        HIPCHK(hipIpcOpenMemHandle(&p, m, hipIpcMemLazyEnablePeerAccess));
+        S->peer_upper = (u64 *)p;
+        S->upper_ipc = true;
+    }
+    return 0;
+}
+
+int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *h, sdfgen_hip_slab *lower, sdfgen_hip_slab *upper, char *errbuf,
+                                  size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    SlabSession *S = &h->s;
+    if ((S->slab > 0) != (lower != nullptr) || (S->slab < S->nslabs - 1) != (upper != nullptr))
+        return err.set(SDFGEN_HIP_EINVAL, "slab %d of %d needs exactly its existing neighbours", S->slab, S->nslabs);
+    HIPCHK(hipSetDevice(S->device));
+    for (sdfgen_hip_slab *o : {lower, upper}) {
+        if (!o || o->s.device == S->device) continue;
+        int ok = 0;
+        HIPCHK(hipDeviceCanAccessPeer(&ok, S->device, o->s.device));
+        if (!ok) return err.set(SDFGEN_HIP_ERUNTIME, "GPU %d cannot access GPU %d", S->device, o->s.device);
+        hipError_t e = hipDeviceEnablePeerAccess(o->s.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
+        (void)hipGetLastError();
+    }
+    S->peer_lower = lower ? lower->s.inbox_mem : nullptr;
+    S->peer_upper = upper ? upper->s.inbox_mem : nullptr;
+    return 0;
+}
+
+int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *h, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
+                            uint64_t nvert, const float origin[3], float dx, int exact_band, int out_layout,
+                            float *d_phi_slab, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    SlabSession *S = &h->s;
+    int rc = validate(ntri, nvert, dx, S->ni, S->nj, S->nk, out_layout, err);
+    if (rc) return rc;
+    if (!d_phi_slab || !origin || (ntri && (!d_tri || !d_xyz)))
+        return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    std::lock_guard<std::mutex> lk(S->mu);
+    HIPCHK(hipSetDevice(S->device));
+    return slab_enqueue(S, d_tri, ntri, d_xyz, nvert, origin, dx, exact_band, out_layout, d_phi_slab, err);
+}
+
+int sdfgen_hip_slab_finish(sdfgen_hip_slab *h, uint64_t nvert, sdfgen_hip_profile *prof, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    std::lock_guard<std::mutex> lk(h->s.mu);
+    HIPCHK(hipSetDevice(h->s.device));
+    return slab_finish(&h->s, nvert, prof, err);
+}
+
+int sdfgen_hip_slab_run(sdfgen_hip_slab *h, const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert,
+                        const float origin[3], float dx, int exact_band, int out_layout, float *phi_slab,
+                        sdfgen_hip_profile *prof, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    SlabSession *S = &h->s;
+    int rc = validate(ntri, nvert, dx, S->ni, S->nj, S->nk, out_layout, err);
+    if (rc) return rc;
+    if (!phi_slab || !origin || (ntri && (!tri || !xyz))) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    std::lock_guard<std::mutex> lk(S->mu);
+    HIPCHK(hipSetDevice(S->device));
+    const uint64_t nout = (uint64_t)S->ni * S->nj * (S->k_end - S->k_begin);
+    auto grow_raw = [&](auto **p, size_t *cap, size_t bytes) -> int {
+        if (*p && *cap >= bytes) return 0;
+        if (*p) HIPCHK(hipFree(*p));
+        *p = nullptr;
+        *cap = 0;
+        HIPCHK(hipMalloc((void **)p, std::max<size_t>(bytes, 16)));
+        *cap = bytes;
+        return 0;
+    };
+    if ((rc = grow_raw(&S->tri, &S->cap_tri, 12 * ntri))) return rc;
+    if ((rc = grow_raw(&S->xyz, &S->cap_xyz, 12 * nvert))) return rc;
+    if ((rc = grow_raw(&S->out, &S->cap_out, 4 * nout))) return rc;
+    if (ntri) HIPCHK(hipMemcpyAsync(S->tri, tri, 12 * ntri, hipMemcpyHostToDevice, S->stream));
+    if (nvert) HIPCHK(hipMemcpyAsync(S->xyz, xyz, 12 * nvert, hipMemcpyHostToDevice, S->stream));
+    if ((rc = slab_enqueue(S, S->tri, ntri, S->xyz, nvert, origin, dx, exact_band, out_layout, S->out, err)))
+        return rc;
+    HIPCHK(hipMemcpyAsync(phi_slab, S->out, 4 * nout, hipMemcpyDeviceToHost, S->stream));
+    return slab_finish(S, nvert, prof, err);
+}
+
+int sdfgen_hip_slab_destroy(sdfgen_hip_slab *h)
+{
+    if (!h) return 0;
+    slab_free(&h->s);
+    delete h;
     return 0;
 }
 

@@ -40,6 +40,7 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "geom.hpp"
@@ -107,7 +108,34 @@ struct StParams {
     unsigned char *lc;            // optional: last sweep (+1) in which each cell's label changed
     int sweep;
     int lead;                     // max steps wave w may run ahead of wave w+1 (<= ST_LEAD)
+    // Z-slab mode (one GPU per slab of the grid).  Tiles cover oriented c in
+    // [cs, ce); the plane c = cs-1 of an upstream slab arrives in hc_in, and this slab's plane
+    // c = ce-1 is published to the downstream slab's inbox hc_out.  An inbox holds one granule
+    // per cell (a, b) of the plane, a and b in [-1, A) x [-1, B): index (b+1)*(A+1) + a+1.
+    int cs, ce;
+    const unsigned long long *hc_in;
+    unsigned long long *hc_out;
 };
+
+__device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
+{
+    return (size_t)(b + 1) * (size_t)(P.A + 1) + (size_t)(a + 1);
+}
+
+// label of a granule published for this sweep (bounded spin; error bit 4 on timeout)
+__device__ __forceinline__ int st_inbox_label(const StParams &P, const unsigned long long *p)
+{
+    for (unsigned spins = 0;; ++spins) {
+        const unsigned long long g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if ((uint32_t)(g >> 32) == P.epoch) return (int)(uint32_t)g;
+        if (spins > ST_WATCHDOG) {
+            atomicOr(P.err, 4);
+            atomicMax(P.err + 1, P.sweep + 1);
+            return -1;
+        }
+        __builtin_amdgcn_s_sleep(4);
+    }
+}
 
 __device__ __forceinline__ size_t st_phys(const StParams &P, int a, int b, int c)
 {
@@ -150,8 +178,12 @@ __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v
     }
 }
 
+// SLAB: halo granules may come from another GPU (IPC-mapped inbox), so granule loads
+// and stores are made at system scope; the single-GPU build keeps agent scope.
+template <bool SLAB>
 __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams P)
 {
+    constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
     __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
     __shared__ float s_d[ST_NCW][7 * ST_CPW];      // per compute wave: distance of candidate q for lane
@@ -166,6 +198,17 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     const int L = tid & 63;
     unsigned long long n_evals = 0, n_cpoll = 0, n_hpoll = 0, n_cpoll_own = 0;
 
+    if (SLAB && P.hc_out) {
+        // publish this slab's last plane's face cells (a = -1 or b = -1; constant during the
+        // sweep) to the downstream slab before any task runs
+        const int nf = P.A + 1 + P.B;
+        for (int f = blockIdx.x * ST_THREADS + tid; f < nf; f += gridDim.x * ST_THREADS) {
+            const int a = f <= P.A ? f - 1 : -1, b = f <= P.A ? -1 : f - (P.A + 1);
+            const unsigned t = (uint32_t)P.cell[st_phys(P, a, b, P.ce - 1)];
+            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), ((unsigned long long)P.epoch << 32) | t,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     for (;;) {
         if (tid == 0) s_task = atomicAdd(P.queue, 1);
         __syncthreads();
@@ -173,7 +216,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         if (task >= P.ntasks) break;
         const int2 JK = P.tasks[task];
         const int J = JK.x, K = JK.y;
-        const int b0 = J * ST_T, c0 = K * ST_T;
+        const int b0 = J * ST_T, c0 = P.cs + K * ST_T;
+        const bool inbox = SLAB && K == 0 && P.hc_in != nullptr;   // c0-1 lives on the upstream GPU
         const int nsteps = P.A + 2 * (ST_T - 1);
 
         // ---------------- task setup, then one barrier ----------------
@@ -184,7 +228,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 const int b = b0 + bl, c = c0 + cl;
                 float4 v0, v1, v2;
                 int t = -1;
-                if (b < P.B && c < P.C) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
+                if (b < P.B && c < P.ce) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
                 st_load_tri(P.soup, t, v0, v1, v2);
                 const int e = ST_RING0 + (ST_RR - 1) * ST_NCOL + cl * ST_T + bl;
                 s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
@@ -199,12 +243,15 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         } else if (L < ST_NSTREAM) {
             int hb_ = 0, hc_ = 0;
             bool valid;
-            if (L < ST_T) { hb_ = b0 - 1; hc_ = c0 + L; valid = hc_ < P.C; }
+            if (L < ST_T) { hb_ = b0 - 1; hc_ = c0 + L; valid = hc_ < P.ce; }
             else if (L < 2 * ST_T) { hb_ = b0 + (L - ST_T); hc_ = c0 - 1; valid = hb_ < P.B; }
             else { hb_ = b0 - 1; hc_ = c0 - 1; valid = true; }
             float4 v0, v1, v2;
             int t = -1;
-            if (valid) t = (int)(uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
+            if (valid) {
+                if (inbox && L >= ST_T) t = st_inbox_label(P, P.hc_in + st_inbox(P, -1, hb_));
+                else t = (int)(uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
+            }
             st_load_tri(P.soup, t, v0, v1, v2);
             const int e = ST_HALO0 + L * ST_RH + (ST_RH - 1);
             s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
@@ -225,7 +272,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             const int bl = L & (ST_T - 1), cl = ST_CLW * w + ((L >> 3) & (ST_CLW - 1));
             const int col_id = cl * ST_T + bl;
             const int b = b0 + bl, c = c0 + cl;
-            const bool col = cell_lane && b < P.B && c < P.C;
+            const bool col = cell_lane && b < P.B && c < P.ce;
             __builtin_amdgcn_s_setprio(2);
             int nb_base[7], nb_stride[7], nb_mask[7];
             {
@@ -274,7 +321,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     ++n_cpoll;
                     if (!__all(own_ok)) ++n_cpoll_own;
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
-                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); }
+                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
                         h = nsteps;
                         break;
                     }
@@ -394,11 +441,12 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                     const unsigned long long gran = ((unsigned long long)P.epoch << 32) | (uint32_t)ct;
                     if (bl == ST_T - 1 && J < P.nJ - 1)
-                        __hip_atomic_store(P.hb + ((size_t)J * P.C + c) * P.A + a, gran, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(P.hb + ((size_t)J * P.C + c) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
                     if (cl == ST_T - 1 && K < P.nK - 1)
-                        __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                    if (SLAB && P.hc_out && c == P.ce - 1)
+                        __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
                 }
                 if (P.trace) {
                     t_comp += wall_clock64() - tc0;
@@ -420,7 +468,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         } else {
             const int bl = L & (ST_T - 1), cl = L >> 3;   // helper lane L prefetches column (bl, cl)
             const int b = b0 + bl, c = c0 + cl;
-            const bool col = b < P.B && c < P.C;
+            const bool col = b < P.B && c < P.ce;
             // ======================= helper wave =======================
             // stream geometry (lanes < 17)
             const bool hlane = L < ST_NSTREAM;
@@ -429,14 +477,18 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             const unsigned long long *hsrc = nullptr;
             if (hlane) {
                 if (L < ST_T) {
-                    hbs = b0 - 1; hcs = c0 + L; hoff = L; hvalid = hcs < P.C; hbound = (J == 0);
+                    hbs = b0 - 1; hcs = c0 + L; hoff = L; hvalid = hcs < P.ce; hbound = (J == 0);
                     if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
                 } else if (L < 2 * ST_T) {
-                    hbs = b0 + (L - ST_T); hcs = c0 - 1; hoff = L - ST_T; hvalid = hbs < P.B; hbound = (K == 0);
-                    if (!hbound) hsrc = P.hc + ((size_t)(K - 1) * P.B + hbs) * P.A;
+                    hbs = b0 + (L - ST_T); hcs = c0 - 1; hoff = L - ST_T; hvalid = hbs < P.B;
+                    hbound = (K == 0) && !inbox;
+                    if (inbox) hsrc = P.hc_in + st_inbox(P, 0, hbs);
+                    else if (!hbound) hsrc = P.hc + ((size_t)(K - 1) * P.B + hbs) * P.A;
                 } else {
-                    hbs = b0 - 1; hcs = c0 - 1; hoff = 0; hvalid = true; hbound = (J == 0 || K == 0);
-                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
+                    hbs = b0 - 1; hcs = c0 - 1; hoff = 0; hvalid = true;
+                    hbound = (J == 0 || K == 0) && !inbox;
+                    if (inbox) hsrc = P.hc_in + st_inbox(P, 0, hbs);
+                    else if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
                 }
             }
             if (!hvalid || hbound) hsrc = P.hb;   // any valid address: unused lanes load harmlessly
@@ -503,7 +555,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         cn = P.cell[ok_ ? st_phys(P, a_, b, c) : dummy];                                               \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + dummy : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g)); \
-        qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                      \
+        qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE);                                        \
     }
                 // Always issued (a fixed count keeps the waits below precise); slots with nothing
                 // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
@@ -557,7 +609,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
                     ++n_hpoll;
                     if (++idle > ST_WATCHDOG) {
-                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); }
+                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
                         break;
                     }
                     if (idle < 4) __builtin_amdgcn_s_sleep(1);
@@ -587,9 +639,13 @@ struct TileSweepWorkspace {
     int grid_override = 0;     // diagnostics: cap on resident workgroups
     int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
     size_t cap_hb = 0, cap_hc = 0;
-    int2 *tasks = nullptr;
-    size_t cap_tasks = 0;
-    int task_nJ = -1, task_nK = -1;
+    // task tables (dequeue order) for up to two tile grids: a Z-slab alternates between
+    // two c extents (k-up and k-down sweeps), and a table must not be rewritten while a
+    // kernel still on the stream reads it
+    int2 *tasks[2] = {nullptr, nullptr};
+    size_t cap_tasks[2] = {0, 0};
+    int task_nJ[2] = {-1, -1}, task_nK[2] = {-1, -1};
+    int task_next = 0;
     int *ctrl = nullptr;   // [0] queue counter, [1] error bits
     unsigned epoch = 0;
     bool count = false;
@@ -610,18 +666,29 @@ inline int st_grow(unsigned long long **p, size_t *cap, size_t need)
     return 0;
 }
 
+// Z-slab part of one sweep: oriented c range of this slab and its inboxes.
+struct TileSlab {
+    bool on = false;
+    int cs = 0, ce = 0;                       // this slab's oriented c range
+    const unsigned long long *in = nullptr;   // inbox: plane cs-1 from the upstream slab (null: first)
+    unsigned long long *out = nullptr;        // downstream slab's inbox for plane ce-1 (null: last)
+};
+
 // Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
-                      unsigned char *lc, const float origin[3], float dx, int ni, int nj, int nk, int di, int dj, int dk, char *err,
-                      size_t errlen)
+                      unsigned char *lc, const float origin[3], float dx, int ni, int nj, int nk, int di, int dj,
+                      int dk, char *err, size_t errlen, const TileSlab &slab = TileSlab())
 {
     const int A = ni - 1, B = nj - 1, C = nk - 1;
-    const int nJ = (B + ST_T - 1) / ST_T, nK = (C + ST_T - 1) / ST_T;
+    const int cs = slab.on ? slab.cs : 0, ce = slab.on ? slab.ce : C;
+    const int nJ = (B + ST_T - 1) / ST_T, nK = (ce - cs + ST_T - 1) / ST_T;
     const int ntasks = nJ * nK;
     auto fail = [&](int code, const char *msg) {
         if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
         return code;
     };
+    // buffers only grow; replacing one while an earlier launch may still use it needs a sync
+    if (W.cap_hb < (size_t)nJ * C * A || W.cap_hc < (size_t)nK * B * A) (void)hipStreamSynchronize(st);
     if (st_grow(&W.hb, &W.cap_hb, (size_t)nJ * C * A)) return fail(-5, "halo buffer allocation failed");
     if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A)) return fail(-5, "halo buffer allocation failed");
     if (!W.ctrl) {
@@ -629,7 +696,11 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
         if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
         if (hipMemset(W.ctrl, 0, 16 * sizeof(int)) != hipSuccess) return fail(-4, "memset");
     }
-    if (W.task_nJ != nJ || W.task_nK != nK) {
+    int ti = (W.task_nJ[0] == nJ && W.task_nK[0] == nK) ? 0 : (W.task_nJ[1] == nJ && W.task_nK[1] == nK) ? 1 : -1;
+    if (ti < 0) {
+        ti = W.task_next;
+        W.task_next ^= 1;
+        (void)hipStreamSynchronize(st);   // the slot being replaced may still be read by a running launch
         std::vector<int2> t;
         t.reserve(ntasks);
         for (int d = 0; d <= nJ + nK - 2; ++d)
@@ -637,15 +708,18 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
                 const int K = d - J;
                 if (K >= 0 && K < nK) t.push_back(make_int2(J, K));
             }
-        if ((size_t)ntasks > W.cap_tasks) {
-            if (W.tasks) (void)hipFree(W.tasks);
-            if (hipMalloc((void **)&W.tasks, ntasks * sizeof(int2)) != hipSuccess) return fail(-5, "task table");
-            W.cap_tasks = ntasks;
+        if ((size_t)ntasks > W.cap_tasks[ti]) {
+            if (W.tasks[ti]) (void)hipFree(W.tasks[ti]);
+            W.tasks[ti] = nullptr;
+            W.cap_tasks[ti] = 0;
+            if (hipMalloc((void **)&W.tasks[ti], std::max(ntasks, 1) * sizeof(int2)) != hipSuccess)
+                return fail(-5, "task table");
+            W.cap_tasks[ti] = std::max(ntasks, 1);
         }
-        if (hipMemcpy(W.tasks, t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess)
+        if (ntasks && hipMemcpy(W.tasks[ti], t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess)
             return fail(-4, "task table upload");
-        W.task_nJ = nJ;
-        W.task_nK = nK;
+        W.task_nJ[ti] = nJ;
+        W.task_nK[ti] = nK;
     }
     if (++W.epoch == 0) ++W.epoch;
     if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
@@ -654,7 +728,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.cell = cell;
     P.hb = W.hb;
     P.hc = W.hc;
-    P.tasks = W.tasks;
+    P.tasks = W.tasks[ti];
     P.queue = W.ctrl;
     P.err = W.ctrl + 1;
     P.stats = W.count ? W.stats : nullptr;
@@ -683,17 +757,23 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.lc = lc;
     P.sweep = W.cur_sweep;
     P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
+    P.cs = cs;
+    P.ce = ce;
+    P.hc_in = slab.on ? slab.in : nullptr;
+    P.hc_out = slab.on ? slab.out : nullptr;
+    if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
     if (getenv("SDFGEN_OCC")) {   // diagnostics: resident workgroups per CU
         int occ = -1;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sweep_tile, ST_THREADS, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sweep_tile<false>, ST_THREADS, 0);
         hipFuncAttributes fa;
-        (void)hipFuncGetAttributes(&fa, (const void *)k_sweep_tile);
+        (void)hipFuncGetAttributes(&fa, (const void *)k_sweep_tile<false>);
         fprintf(stderr, "k_sweep_tile: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", occ, fa.numRegs,
                 fa.sharedSizeBytes, fa.localSizeBytes);
     }
-    hipLaunchKernelGGL(k_sweep_tile, dim3(grid), dim3(ST_THREADS), 0, st, P);
+    if (slab.on) hipLaunchKernelGGL(k_sweep_tile<true>, dim3(grid), dim3(ST_THREADS), 0, st, P);
+    else hipLaunchKernelGGL(k_sweep_tile<false>, dim3(grid), dim3(ST_THREADS), 0, st, P);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }
@@ -702,7 +782,8 @@ inline void tile_sweep_release(TileSweepWorkspace &W)
 {
     (void)hipFree(W.hb);
     (void)hipFree(W.hc);
-    (void)hipFree(W.tasks);
+    (void)hipFree(W.tasks[0]);
+    (void)hipFree(W.tasks[1]);
     (void)hipFree(W.ctrl);
     (void)hipFree(W.stats);
     (void)hipFree(W.trace);

@@ -1,0 +1,143 @@
+"""Z-slab decomposition (sdfgen_hip_slab_*) -- bit-exact against the oracle.
+
+Slabs of one grid run concurrently on ONE GPU here (the box has one), either in one
+process (connect_local, one HIP stream per slab) or one process per slab with the
+inboxes mapped through HIP IPC (the 8-GPU layout, minus xGMI).  Every slab's tile
+kernel is capped (SDFGEN_TILE_GRID) so that all slabs' workgroups are resident at
+once -- on separate GPUs nothing is shared and no cap is needed.
+"""
+import multiprocessing as mp
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import bits_equal, diff_report
+from oracle import oracle as O
+from sdfgen_amd import meshgen
+
+pytestmark = pytest.mark.gpu
+
+
+def _mesh(nu=90, nv=31, dims=(40, 36, 44)):
+    v, t = meshgen.bumpy_sphere(nu, nv)
+    o, dx = meshgen.grid_mode2b(v, *(max(d, 8) for d in dims), 2)   # small grids: a crop of an 8^3 layout
+    return v, t, o, dx, dims
+
+
+@pytest.fixture(autouse=True)
+def _cap_grid(monkeypatch):
+    monkeypatch.setenv("SDFGEN_TILE_GRID", "96")
+
+
+# In one process every slab needs its own hardware queue (a consumer kernel spinning in
+# a queue shared with its producer would wait forever); GPU_MAX_HW_QUEUES is 4 on the box,
+# so in-process tests use 2 slabs and the 3-4 slab layouts run one process per slab.
+@pytest.mark.parametrize("nslabs,dims", [(2, (40, 36, 44)), (2, (33, 41, 29)), (2, (9, 9, 4)), (2, (17, 5, 60))])
+def test_slabs_one_process_match_oracle(nslabs, dims):
+    from sdfgen_amd import _hiprt, _lib
+    v, t, o, dx, dims = _mesh(dims=dims)
+    ni, nj, nk = dims
+    want = np.asfortranarray(O.make_level_set3(v, t, o, dx, ni, nj, nk, 1))
+    slabs = [_lib.Slab(0, nslabs, s, ni, nj, nk) for s in range(nslabs)]
+    for s, sl in enumerate(slabs):
+        sl.connect_local(slabs[s - 1] if s > 0 else None, slabs[s + 1] if s < nslabs - 1 else None)
+    dv, dt = _hiprt.DeviceBuffer.from_array(v), _hiprt.DeviceBuffer.from_array(t)
+    outs = [_hiprt.DeviceBuffer(ni * nj * (sl.k_end - sl.k_begin) * 4) for sl in slabs]
+    for sl, d in zip(slabs, outs):
+        sl.enqueue(dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx, 1, _lib.LAYOUT_ARRAY3, d.ptr)
+    profs = [sl.finish(v.shape[0]) for sl in slabs]
+    got = np.concatenate([d.download(np.float32, ni * nj * (sl.k_end - sl.k_begin)) for sl, d in zip(slabs, outs)])
+    got = got.reshape((ni, nj, nk), order="F")
+    assert [sl.k_begin for sl in slabs][0] == 0 and slabs[-1].k_end == nk
+    assert all(p["sweep_impl"] == 3 for p in profs)
+    assert bits_equal(got, want), diff_report(got, want, dx)
+
+
+def test_slab_kfast_layout_and_host_run():
+    from sdfgen_amd import _lib
+    v, t, o, dx, dims = _mesh()
+    ni, nj, nk = dims
+    want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, ni, nj, nk, 1))
+    slabs = [_lib.Slab(0, 2, s, ni, nj, nk) for s in range(2)]
+    slabs[0].connect_local(None, slabs[1])
+    slabs[1].connect_local(slabs[0], None)
+    # host-array entry runs one slab at a time: run slab 0's producer side by enqueueing
+    # the device path for slab 1 first is not possible with run(); use enqueue for both
+    from sdfgen_amd import _hiprt
+    dv, dt = _hiprt.DeviceBuffer.from_array(v), _hiprt.DeviceBuffer.from_array(t)
+    outs = [_hiprt.DeviceBuffer(ni * nj * (sl.k_end - sl.k_begin) * 4) for sl in slabs]
+    for sl, d in zip(slabs, outs):
+        sl.enqueue(dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx, 1, _lib.LAYOUT_KFAST, d.ptr)
+    for sl in slabs:
+        sl.finish()
+    parts = [d.download(np.float32, ni * nj * (sl.k_end - sl.k_begin)).reshape(ni, nj, sl.k_end - sl.k_begin)
+             for sl, d in zip(slabs, outs)]
+    got = np.concatenate(parts, axis=2)
+    assert bits_equal(got, want), diff_report(got, want, dx)
+
+
+def test_slab_validation():
+    from sdfgen_amd import _lib
+    with pytest.raises(ValueError):
+        _lib.Slab(0, 3, 0, 10, 10, 5)      # fewer than 2 planes per slab
+    with pytest.raises(ValueError):
+        _lib.Slab(0, 2, 2, 10, 10, 10)     # slab index out of range
+    s = _lib.Slab(0, 2, 0, 10, 10, 10)
+    with pytest.raises(ValueError):
+        s.connect_local(None, None)        # slab 0 of 2 needs its upper neighbour
+
+
+def _ipc_worker(nslabs, slab, dims, q_out, q_in, barrier, res):
+    os.environ["SDFGEN_TILE_GRID"] = "64"
+    from sdfgen_amd import _lib
+    v, t, o, dx, dims = _mesh(dims=dims)
+    sl = _lib.Slab(0, nslabs, slab, *dims)
+    q_out.put((slab, sl.export()))
+    handles = q_in.get(timeout=120)
+    sl.connect_ipc(handles.get(slab - 1), handles.get(slab + 1))
+    barrier.wait(timeout=120)
+    phi, prof = sl.run(v, t, o, dx, 1, _lib.LAYOUT_ARRAY3)
+    res.put((slab, sl.k_begin, sl.k_end, np.asfortranarray(phi).tobytes(order="F"), prof["sweep_impl"]))
+    barrier.wait(timeout=120)   # keep the inbox mapped until every peer has finished writing
+    sl.close()
+
+
+@pytest.mark.parametrize("nslabs,dims", [(3, (33, 41, 29)), (4, (24, 20, 17)), (3, (8, 70, 6))])
+def test_slabs_middle_slabs_in_process(nslabs, dims):
+    """Slabs with both an upstream and a downstream neighbour; one HW queue per slab stream."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8", SDFGEN_TILE_GRID="64")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"),
+                        str(nslabs), *map(str, dims)], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr[-3000:]
+
+
+# One process per slab, inboxes mapped with HIP IPC.  Two processes only: more processes
+# sharing one GPU's hardware queues are not guaranteed to run their kernels concurrently.
+@pytest.mark.parametrize("nslabs,dims", [(2, (40, 36, 44)), (2, (19, 23, 31))])
+def test_slabs_ipc_one_process_per_slab_match_oracle(nslabs, dims):
+    ctx = mp.get_context("spawn")
+    q_out, res, barrier = ctx.Queue(), ctx.Queue(), ctx.Barrier(nslabs)
+    q_ins = [ctx.Queue() for _ in range(nslabs)]
+    procs = [ctx.Process(target=_ipc_worker, args=(nslabs, s, dims, q_out, q_ins[s], barrier, res))
+             for s in range(nslabs)]
+    for p in procs:
+        p.start()
+    try:
+        handles = dict(q_out.get(timeout=300) for _ in range(nslabs))
+        for q in q_ins:
+            q.put(handles)
+        parts = sorted(res.get(timeout=300) for _ in range(nslabs))
+    finally:
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    v, t, o, dx, (ni, nj, nk) = _mesh(dims=dims)
+    want = np.asfortranarray(O.make_level_set3(v, t, o, dx, ni, nj, nk, 1))
+    got = np.concatenate([np.frombuffer(b, np.float32) for _, _, _, b, _ in parts]).reshape((ni, nj, nk), order="F")
+    assert [p[4] for p in parts] == [3] * nslabs
+    assert bits_equal(got, want), diff_report(got, want, dx)
