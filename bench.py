@@ -5,8 +5,9 @@
 One step = one complete make_level_set3 (prep, band + ray parity, 16 sweeps,
 sign) on the deterministic 1M-triangle bumpy sphere with inputs already
 resident in HBM and phi written to HBM (sdfgen_hip_make_level_set3_device).
-For N > 1 (launched by torch.distributed.run), every rank runs the same
-single-GPU job on its own GPU ("replicas", weak scaling); see DESIGN.md.
+For N > 1 (launched by torch.distributed.run, one rank per GPU) the same grid is
+split into N Z-slabs (sdfgen_amd/distributed.py): each rank owns nk/N planes and the
+sweeps' wavefront runs across the GPUs (strong scaling); see DESIGN.md §7.
 
 Rank 0 prints one JSON line with the driver's contract fields plus
 `roofline` (dominant kernel = the sweep, HIP-event timed inside the library
@@ -68,9 +69,10 @@ def main():
 
     dist = None
     if world > 1:
-        # Control plane only (barrier + max of the wall time): gloo on the host.  The data
-        # path has no collective -- each rank runs an independent job on its own GPU.
-        # torch is imported BEFORE the backend so one HIP runtime serves both (DESIGN.md).
+        # Control plane (IPC-handle exchange, barriers, max of the wall time): gloo on the
+        # host.  The data path is the slab wavefront itself: boundary planes move GPU to GPU
+        # inside the sweep kernels (sdfgen_amd/distributed.py).
+        # torch is imported BEFORE the backend so one HIP runtime serves both (DESIGN.md §8).
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -78,18 +80,29 @@ def main():
 
     from sdfgen_amd import _hiprt, _lib, meshgen
 
-    _hiprt.set_device(local_rank)
+    dev = local_rank % max(_lib.device_count(), 1)   # = local_rank on a node with a GPU per rank
+    _hiprt.set_device(dev)
     v, t, o, dx, dims = meshgen.workload(args.workload)
     ni, nj, nk = dims
     ncell = ni * nj * nk
     dv = _hiprt.DeviceBuffer.from_array(v)
     dt = _hiprt.DeviceBuffer.from_array(t)
-    out = _hiprt.DeviceBuffer(ncell * 4)
+    if world > 1:
+        from sdfgen_amd import distributed as D
+        sess = D._gpu_session(dist, None, dev, dims, world, rank)
+        nks = sess.k_end - sess.k_begin
+        out = _hiprt.DeviceBuffer(ni * nj * nks * 4)
 
-    def step():
-        _lib.make_level_set3_device(local_rank, dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx,
-                                    ni, nj, nk, 1, _lib.LAYOUT_ARRAY3, out.ptr, 0)
-        return _lib.last_profile()
+        def step():
+            sess.enqueue(dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx, 1, _lib.LAYOUT_ARRAY3, out.ptr)
+            return sess.finish(v.shape[0])
+    else:
+        out = _hiprt.DeviceBuffer(ncell * 4)
+
+        def step():
+            _lib.make_level_set3_device(dev, dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx,
+                                        ni, nj, nk, 1, _lib.LAYOUT_ARRAY3, out.ptr, 0)
+            return _lib.last_profile()
 
     def barrier():
         if dist is not None:
@@ -110,7 +123,7 @@ def main():
         el = float(x.item())
 
     ms_step = el / args.steps * 1e3
-    value = world * ncell * args.steps / el / 1e6
+    value = ncell * args.steps / el / 1e6   # one whole grid per step (split over the ranks when N > 1)
     # Dominant kernel: the tile-wavefront sweep (k_sweep_tile), one launch per first-pass
     # sweep.  Its per-launch duration is the library's HIP-event time around that launch on
     # the launch stream; algorithmic bytes per launch = 16 B per swept cell.
@@ -120,6 +133,8 @@ def main():
     tile_ms = [sum(p["sweep_launch_ms"][s] for p in profs) / len(profs) for s in range(n_tile)]
     launch_ms = sum(tile_ms) / max(len(tile_ms), 1)
     bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * C
+    if world > 1:   # this rank's slab; the slab sessions run all 16 sweeps as tile wavefronts
+        bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * (sess.k_end - sess.k_begin)
     achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9 if launch_ms > 0 else 0.0
     sparse_ms = [sum(p["sweep_launch_ms"][s] for p in profs) / len(profs) for s in range(n_tile, 16)]
     phases = {k: round(sum(p[k] for p in profs) / len(profs), 4)
@@ -135,14 +150,17 @@ def main():
             traffic, traffic_src = k["hbm_bytes_per_launch"], "profiles/pmc_summary.json"
 
     parity = None
-    if not args.no_verify and rank == 0:
+    if not args.no_verify:
         hp = os.path.join(ROOT, "tests", "golden", "hashes.json")
-        if os.path.exists(hp):
-            rec = json.load(open(hp)).get(args.workload)
-            if rec:
-                got = out.download(np.float32, ncell)
-                ok = hashlib.sha256(got.astype("<f4").tobytes()).hexdigest() == rec["sha256_phi"]
-                parity = "bit-exact vs reference (sha256 of phi)" if ok else "MISMATCH vs reference sha256"
+        rec = json.load(open(hp)).get(args.workload) if os.path.exists(hp) else None
+        got = out.download(np.float32, out.nbytes // 4)
+        if world > 1:   # assemble the slabs on rank 0 (outside the timed region)
+            parts = [None] * world if rank == 0 else None
+            dist.gather_object(got, parts, dst=0)
+            got = np.concatenate(parts) if rank == 0 else None
+        if rank == 0 and rec:
+            ok = hashlib.sha256(got.astype("<f4").tobytes()).hexdigest() == rec["sha256_phi"]
+            parity = "bit-exact vs reference (sha256 of phi)" if ok else "MISMATCH vs reference sha256"
 
     if rank == 0:
         res = {
@@ -154,12 +172,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (deterministic 1M-triangle bumpy UV-sphere, sdfgen_amd/meshgen.py)",
             "config": {"workload": args.workload, "grid": list(dims), "triangles": int(t.shape[0]),
-                       "exact_band": 1, "parallelism": "replicas" if world > 1 else "single-gpu",
+                       "exact_band": 1, "parallelism": f"zslab{world}" if world > 1 else "single-gpu",
                        "inputs": "HBM-resident"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,

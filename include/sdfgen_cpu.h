@@ -24,6 +24,23 @@ int sdfgen_cpu_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
                                const float origin[3], float dx, int ni, int nj, int nk, int exact_band,
                                int num_threads, int out_layout, float *phi_out, char *errbuf, size_t errlen);
 
+/* Z-slab sessions on the CPU (multi-process runs without GPUs): the same slab split as
+ * sdfgen_hip_slab_* (slab s of n owns k in [s*nk/n, (s+1)*nk/n)).  Per sweep the caller
+ * hands in the upstream slab's final boundary plane and forwards this slab's last plane
+ * (ni*nj packed cells each: phi bits << 32 | closest triangle).  Upstream = the slab
+ * below for k-up sweeps, above for k-down sweeps.  Bit-identical to the whole-grid run. */
+typedef struct sdfgen_cpu_slab sdfgen_cpu_slab;
+int sdfgen_cpu_slab_create(int nslabs, int slab, int ni, int nj, int nk, sdfgen_cpu_slab **out, char *errbuf,
+                           size_t errlen);
+int sdfgen_cpu_slab_range(const sdfgen_cpu_slab *s, int *k_begin, int *k_end);
+/* tri/xyz must stay alive until the last sweep */
+int sdfgen_cpu_slab_band(sdfgen_cpu_slab *s, const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert,
+                         const float origin[3], float dx, int exact_band, char *errbuf, size_t errlen);
+int sdfgen_cpu_slab_sweep(sdfgen_cpu_slab *s, int sweep, const uint64_t *plane_in, uint64_t *plane_out,
+                          char *errbuf, size_t errlen);
+int sdfgen_cpu_slab_sign(sdfgen_cpu_slab *s, int out_layout, float *phi_slab, char *errbuf, size_t errlen);
+int sdfgen_cpu_slab_destroy(sdfgen_cpu_slab *s);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,12 @@ EXPORTED = (
     "sdfgen_hip_slab_finish",
     "sdfgen_hip_slab_run",
     "sdfgen_hip_slab_destroy",
+    "sdfgen_cpu_slab_create",
+    "sdfgen_cpu_slab_range",
+    "sdfgen_cpu_slab_band",
+    "sdfgen_cpu_slab_sweep",
+    "sdfgen_cpu_slab_sign",
+    "sdfgen_cpu_slab_destroy",
 )
 IPC_HANDLE_BYTES = 64
 
@@ -117,6 +123,14 @@ def _load():
     L.sdfgen_hip_slab_destroy.argtypes = [_P]
     for f in ("create", "range", "export", "connect_ipc", "connect_local", "enqueue", "finish", "run", "destroy"):
         getattr(L, "sdfgen_hip_slab_" + f).restype = ctypes.c_int
+    L.sdfgen_cpu_slab_create.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(_P)] + _E
+    L.sdfgen_cpu_slab_range.argtypes = [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.sdfgen_cpu_slab_band.argtypes = [_P, _P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int] + _E
+    L.sdfgen_cpu_slab_sweep.argtypes = [_P, ctypes.c_int, _P, _P] + _E
+    L.sdfgen_cpu_slab_sign.argtypes = [_P, ctypes.c_int, _P] + _E
+    L.sdfgen_cpu_slab_destroy.argtypes = [_P]
+    for f in ("create", "range", "band", "sweep", "sign", "destroy"):
+        getattr(L, "sdfgen_cpu_slab_" + f).restype = ctypes.c_int
     return L
 
 
@@ -312,6 +326,73 @@ class Slab:
     def close(self) -> None:
         if getattr(self, "h", None):
             lib.sdfgen_hip_slab_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class CpuSlab:
+    """CPU Z-slab session (sdfgen_cpu_slab_*); sweeps one at a time with explicit planes."""
+
+    SWEEP_DIRS = ((1, 1, 1), (-1, -1, -1), (1, 1, -1), (-1, -1, 1), (1, -1, 1), (-1, 1, -1), (1, -1, -1), (-1, 1, 1))
+
+    def __init__(self, nslabs: int, slab: int, ni: int, nj: int, nk: int):
+        self.dims = (int(ni), int(nj), int(nk))
+        self.nslabs, self.slab = int(nslabs), int(slab)
+        h = _P()
+        err = ctypes.create_string_buffer(512)
+        rc = lib.sdfgen_cpu_slab_create(self.nslabs, self.slab, *self.dims, ctypes.byref(h), err, ctypes.sizeof(err))
+        if rc != OK:
+            _raise(rc, err)
+        self.h = h
+        kb, ke = ctypes.c_int(), ctypes.c_int()
+        lib.sdfgen_cpu_slab_range(self.h, ctypes.byref(kb), ctypes.byref(ke))
+        self.k_begin, self.k_end = kb.value, ke.value
+
+    def band(self, vertices, triangles, origin, dx: float, exact_band: int = 1) -> None:
+        self._v = np.ascontiguousarray(vertices, dtype=np.float32)   # kept alive for the sweeps
+        self._t = np.ascontiguousarray(triangles, dtype=np.uint32)
+        o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+        err = ctypes.create_string_buffer(512)
+        rc = lib.sdfgen_cpu_slab_band(self.h, self._t.ctypes.data_as(_P), self._t.size // 3,
+                                      self._v.ctypes.data_as(_P), self._v.size // 3, o.ctypes.data_as(_P),
+                                      ctypes.c_float(dx), int(exact_band), err, ctypes.sizeof(err))
+        if rc != OK:
+            _raise(rc, err)
+
+    def upstream_is_below(self, sweep: int) -> bool:
+        return self.SWEEP_DIRS[sweep % 8][2] > 0
+
+    def sweep(self, sweep: int, plane_in: np.ndarray | None, want_out: bool) -> np.ndarray | None:
+        ni, nj, _ = self.dims
+        pin = None if plane_in is None else np.ascontiguousarray(plane_in, dtype=np.uint64)
+        pout = np.empty(ni * nj, dtype=np.uint64) if want_out else None
+        err = ctypes.create_string_buffer(512)
+        rc = lib.sdfgen_cpu_slab_sweep(self.h, int(sweep), None if pin is None else pin.ctypes.data_as(_P),
+                                       None if pout is None else pout.ctypes.data_as(_P), err, ctypes.sizeof(err))
+        if rc != OK:
+            _raise(rc, err)
+        return pout
+
+    def sign(self, layout: int = LAYOUT_ARRAY3) -> np.ndarray:
+        ni, nj, _ = self.dims
+        nks = self.k_end - self.k_begin
+        out = np.empty(ni * nj * nks, dtype=np.float32)
+        err = ctypes.create_string_buffer(512)
+        rc = lib.sdfgen_cpu_slab_sign(self.h, int(layout), out.ctypes.data_as(_P), err, ctypes.sizeof(err))
+        if rc != OK:
+            _raise(rc, err)
+        if layout == LAYOUT_KFAST:
+            return out.reshape((ni, nj, nks))
+        return out.reshape((ni, nj, nks), order="F")
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib.sdfgen_cpu_slab_destroy(self.h)
             self.h = None
 
     def __del__(self):
