@@ -33,6 +33,15 @@ struct f3 {
 };
 
 SDF_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+// Low word of a device cell / granule: the closest triangle in 27 bits (all ones = none)
+// and, in the top 5 bits, the sweep (+1) in which the cell took that label (0 = band).
+// The sweeps' "already examined" skip reads the latter (sweep_sparse.hpp); the band's
+// atomicMin keys (phi << 32 | t) are unchanged by it.  Limits meshes to 2^27-1 triangles.
+constexpr uint32_t LBL_BITS = 27u, LBL_MASK = (1u << LBL_BITS) - 1u;
+SDF_HD int lbl_of(uint32_t w) { const uint32_t l = w & LBL_MASK; return l == LBL_MASK ? -1 : (int)l; }
+SDF_HD int lc_of(uint32_t w) { return (int)(w >> LBL_BITS); }
+SDF_HD uint32_t lo_word(int label, int lc) { return ((uint32_t)lc << LBL_BITS) | ((uint32_t)label & LBL_MASK); }
 SDF_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 
 SDF_HD f3 mk3(float x, float y, float z) { return f3{x, y, z}; }

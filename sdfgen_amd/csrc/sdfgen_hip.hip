@@ -190,16 +190,16 @@ __device__ __forceinline__ void sweep_cell(const float4 *__restrict__ soup, u64 
     const size_t c0 = cidx(i, j, k, g.ni, g.nj);
     const u64 own = cell[c0];
     float phi = __uint_as_float((uint32_t)(own >> 32));
-    int32_t ct = (int32_t)(uint32_t)own;
+    int32_t ct = lbl_of((uint32_t)own);
     const int32_t ct_orig = ct;
     int32_t nb[7];
-    nb[0] = (int32_t)(uint32_t)cell[cidx(i - di, j, k, g.ni, g.nj)];
-    nb[1] = (int32_t)(uint32_t)cell[cidx(i, j - dj, k, g.ni, g.nj)];
-    nb[2] = (int32_t)(uint32_t)cell[cidx(i - di, j - dj, k, g.ni, g.nj)];
-    nb[3] = (int32_t)(uint32_t)cell[cidx(i, j, k - dk, g.ni, g.nj)];
-    nb[4] = (int32_t)(uint32_t)cell[cidx(i - di, j, k - dk, g.ni, g.nj)];
-    nb[5] = (int32_t)(uint32_t)cell[cidx(i, j - dj, k - dk, g.ni, g.nj)];
-    nb[6] = (int32_t)(uint32_t)cell[cidx(i - di, j - dj, k - dk, g.ni, g.nj)];
+    nb[0] = lbl_of((uint32_t)cell[cidx(i - di, j, k, g.ni, g.nj)]);
+    nb[1] = lbl_of((uint32_t)cell[cidx(i, j - dj, k, g.ni, g.nj)]);
+    nb[2] = lbl_of((uint32_t)cell[cidx(i - di, j - dj, k, g.ni, g.nj)]);
+    nb[3] = lbl_of((uint32_t)cell[cidx(i, j, k - dk, g.ni, g.nj)]);
+    nb[4] = lbl_of((uint32_t)cell[cidx(i - di, j, k - dk, g.ni, g.nj)]);
+    nb[5] = lbl_of((uint32_t)cell[cidx(i, j - dj, k - dk, g.ni, g.nj)]);
+    nb[6] = lbl_of((uint32_t)cell[cidx(i - di, j - dj, k - dk, g.ni, g.nj)]);
     const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
     bool changed = false;
 #pragma unroll
@@ -218,7 +218,7 @@ __device__ __forceinline__ void sweep_cell(const float4 *__restrict__ soup, u64 
             }
         }
     }
-    if (changed) cell[c0] = ((u64)__float_as_uint(phi) << 32) | (u64)(uint32_t)ct;
+    if (changed) cell[c0] = ((u64)__float_as_uint(phi) << 32) | lo_word(ct, 0);
 }
 
 // Reference-order sweep, one launch per oriented hyperplane s = a+b+c:
@@ -306,8 +306,6 @@ struct Workspace {
     hipStream_t stream = nullptr;
     u64 *cell = nullptr;
     uint32_t *cnt = nullptr;
-    unsigned char *lc = nullptr;   // last sweep (+1) that changed each cell's label (sparse sweeps)
-    size_t cap_lc = 0;
     float4 *soup = nullptr;
     uint32_t *tri = nullptr;
     float *xyz = nullptr;
@@ -368,7 +366,8 @@ int validate(uint64_t ntri, uint64_t nvert, float dx, int ni, int nj, int nk, in
     if (layout != SDFGEN_LAYOUT_ARRAY3 && layout != SDFGEN_LAYOUT_KFAST)
         return err.set(SDFGEN_HIP_EINVAL, "out_layout must be 0 (Array3f) or 1 (k-fastest)");
     if ((uint64_t)ni * nj * nk >= (1ull << 40)) return err.set(SDFGEN_HIP_EINVAL, "grid too large");
-    if (ntri > 0x7fffffffull) return err.set(SDFGEN_HIP_EINVAL, "too many triangles (> 2^31-1)");
+    if (ntri >= (uint64_t)LBL_MASK)
+        return err.set(SDFGEN_HIP_EINVAL, "too many triangles (the GPU backend supports up to %u)", LBL_MASK - 1u);
     (void)nvert;
     return 0;
 }
@@ -450,11 +449,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         const char *e = getenv("SDFGEN_SPARSE_WORKERS");   // diagnostics: repair-kernel workgroups
         ws->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
     }
-    if (sparse_first < 16) {
-        if ((rc = grow(&ws->lc, &ws->cap_lc, n, err))) return rc;
-        HIPCHK(hipMemsetAsync(ws->lc, 0, n, st));
-    }
-    unsigned char *lc = sparse_first < 16 ? ws->lc : nullptr;
+    ws->wf.skip_seen = getenv("SDFGEN_NO_SEEN_SKIP") == nullptr;   // diagnostics
     if (ws->wf.ctrl) HIPCHK(hipMemsetAsync(ws->wf.ctrl + 1, 0, sizeof(int), st));   // error bits of this call
     if (sparse_first < 16 && ws->sp.ctl) HIPCHK(hipMemsetAsync(ws->sp.ctl, 0, SP_NCTL * sizeof(u64), st));
     for (int s = 0; s < 16; ++s) {
@@ -462,7 +457,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         if (!do_sweep || s >= nsweeps) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
         if (impl == 1 && s >= sparse_first) {
-            if ((rc = sparse_sweep(ws->sp, st, ws->soup, &ws->cell, &ws->cap_cell, lc, origin, dx, ni, nj, nk, s)))
+            if ((rc = sparse_sweep(ws->sp, st, ws->soup, &ws->cell, &ws->cap_cell, origin, dx, ni, nj, nk, s)))
                 return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU sparse sweep setup failed");
             launches += 2;
             ++sparse_sweeps;
@@ -470,7 +465,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         }
         if (impl == 1) {
             ws->wf.cur_sweep = s;
-            if ((rc = tile_sweep(ws->wf, st, ws->soup, ws->cell, lc, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
+            if ((rc = tile_sweep(ws->wf, st, ws->soup, ws->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
                                       err.len)))
                 return rc;
             ++launches;
@@ -705,7 +700,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
             sl.out = S->peer_lower ? S->peer_lower + S->plane * (2 + par) : nullptr;
         }
         S->wf.cur_sweep = s;
-        int rc = tile_sweep(S->wf, st, S->soup, S->cell, nullptr, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
+        int rc = tile_sweep(S->wf, st, S->soup, S->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
                             err.len, sl);
         if (rc) return rc;
         ++S->launches;
@@ -851,7 +846,6 @@ int sdfgen_hip_release(void)
     for (Workspace *w : g_ws) {
         hipSetDevice(w->device);
         hipFree(w->cell);
-        hipFree(w->lc);
         hipFree(w->cnt);
         hipFree(w->soup);
         hipFree(w->tri);

@@ -56,7 +56,6 @@ struct SpParams {
     unsigned long long *ctl;           // SP_* counters
     unsigned long long cap;            // ring slots
     unsigned long long n;              // cells
-    unsigned char *lc;                 // per cell: 0 = label from the band, s+1 = last changed in sweep s
     float ox, oy, oz, dx;
     int ni, nj, nk;
     int di, dj, dk;
@@ -101,9 +100,9 @@ __device__ __forceinline__ bool sp_in(const SpParams &P, int i, int j, int k)
 // One more exact skip: phi_c always equals d(c, label_c) and only decreases, so once c
 // has examined label L, d(c, L) >= phi_c for ever after.  An interior cell examined
 // neighbour u in the last earlier sweep s' whose direction makes u upwind of c (seen[q]);
-// if u's label has not changed since (lc[u] <= s'+1), c has already seen that label.
-// With LIVE labels (the repair pass) this applies only while u still holds its
-// pre-sweep label, whose change history lc describes.
+// if u's label has not changed since (the sweep stamped in u's low word is <= s'), c has
+// already seen that label.  A label set in this very sweep carries this sweep's stamp,
+// so the LIVE (repair) evaluation needs no extra check.
 template <bool LIVE>
 __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
                                                       int k, size_t c, unsigned long long own)
@@ -111,12 +110,17 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
     const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
     const long long cc = (long long)c;
     const long long nb[7] = {cc - si, cc - sj, cc - si - sj, cc - sk, cc - si - sk, cc - sj - sk, cc - si - sj - sk};
-    int lab[7];
+    int lab[7], lcq[7];
 #pragma unroll
-    for (int q = 0; q < 7; ++q) lab[q] = (int)(uint32_t)(LIVE ? sp_ld64(L + nb[q]) : L[nb[q]]);
+    for (int q = 0; q < 7; ++q) {
+        const uint32_t w = (uint32_t)(LIVE ? sp_ld64(L + nb[q]) : L[nb[q]]);
+        lab[q] = lbl_of(w);
+        lcq[q] = lc_of(w);
+    }
     float phi = __uint_as_float((uint32_t)(own >> 32));
-    int ct = (int)(uint32_t)own;
+    int ct = lbl_of((uint32_t)own);
     const int ct0 = ct;
+    bool changed = false;
     const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
     const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
 #pragma unroll
@@ -125,20 +129,19 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
         bool skip = (t < 0) || (t == ct0);
 #pragma unroll
         for (int r = 0; r < q; ++r) skip = skip || (lab[r] == t);
-        if (!skip && interior && P.seen[q] >= 0) {
-            const bool pre = LIVE ? (int)(uint32_t)P.S[nb[q]] == t : true;
-            if (pre && (int)P.lc[nb[q]] <= P.seen[q]) skip = true;
-        }
+        skip = skip || (interior && lcq[q] <= P.seen[q]);   // seen[q] = -1: never
         if (!skip) {
             const float4 v0 = P.soup[3 * (size_t)t], v1 = P.soup[3 * (size_t)t + 1], v2 = P.soup[3 * (size_t)t + 2];
             const float d = ptd(gx, mk3(v0.x, v0.y, v0.z), mk3(v1.x, v1.y, v1.z), mk3(v2.x, v2.y, v2.z));
             if (d < phi) {
                 phi = d;
                 ct = t;
+                changed = true;
             }
         }
     }
-    return ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
+    if (!changed) return own;
+    return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
 }
 
 __device__ __forceinline__ void sp_enqueue(const SpParams &P, size_t e)
@@ -204,10 +207,7 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
         }
         const unsigned long long y = sp_eval<false>(P, P.S, i, j, k, c, s);
         P.X[c] = y;
-        if ((uint32_t)y != (uint32_t)s) {
-            P.lc[c] = (unsigned char)(P.sweep + 1);
-            sp_request_downstream(P, i, j, k, c, false);
-        }
+        if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) sp_request_downstream(P, i, j, k, c, false);
     }
 }
 
@@ -256,8 +256,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             ++runs;
             if (y != cur) {
                 sp_st64(P.X + e, y);
-                if ((uint32_t)y != (uint32_t)cur) {
-                    P.lc[e] = (unsigned char)(P.sweep + 1);
+                if (lbl_of((uint32_t)y) != lbl_of((uint32_t)cur)) {
                     sp_order();   // the new label is visible before anyone is asked to read it
                     const size_t m = sp_request_downstream(P, i, j, k, e, next == NONE);
                     if (m != NONE) next = m;
@@ -319,7 +318,7 @@ inline int sp_grow(T **p, size_t *cap, size_t need, bool zero)
 // Enqueue one sparse sweep on `st`: reads *cell, writes the other buffer, then swaps
 // the two so *cell holds the result.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long **cell,
-                        size_t *cap_cell, unsigned char *lc, const float origin[3], float dx, int ni, int nj, int nk,
+                        size_t *cap_cell, const float origin[3], float dx, int ni, int nj, int nk,
                         int sweep)
 {
     const int di = SP_DIRS[sweep % 8][0], dj = SP_DIRS[sweep % 8][1], dk = SP_DIRS[sweep % 8][2];
@@ -354,7 +353,6 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     P.di = di;
     P.dj = dj;
     P.dk = dk;
-    P.lc = lc;
     P.sweep = sweep;
     for (int q = 0; q < 7; ++q) {
         const int m = q + 1;   // neighbour slot q lies upwind along the axes in mask m

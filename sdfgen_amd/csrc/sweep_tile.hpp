@@ -90,6 +90,16 @@ constexpr int ST_OWN0 = ST_HALO0 + ST_NSTREAM * ST_RH;        // RO slots x 64 c
 constexpr int ST_ENTS = ST_OWN0 + ST_RO * ST_NCOL;
 constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
 
+// Entry layout in LDS: [3e] = (x1, w), [3e+1] = (x2, phi -- own entries only), [3e+2] = x3,
+// where w is the cell's low word (label and the sweep that set it: geom.hpp lo_word).
+
+// granule = {epoch (32 bits), low word (32 bits)}: the data is the flag
+__device__ __forceinline__ unsigned long long st_granule(unsigned epoch, uint32_t w)
+{
+    return ((unsigned long long)epoch << 32) | w;
+}
+__device__ __forceinline__ bool st_granule_ready(unsigned long long g, unsigned epoch) { return (uint32_t)(g >> 32) == epoch; }
+
 struct StParams {
     const float4 *soup;           // 3 float4 per triangle (xyz; w unused)
     unsigned long long *cell;     // (phi bits << 32) | closest_tri, i-fastest
@@ -105,7 +115,6 @@ struct StParams {
     int A, B, C, nJ, nK, ntasks;
     int di, dj, dk;
     unsigned epoch;
-    unsigned char *lc;            // optional: last sweep (+1) in which each cell's label changed
     int sweep;
     int lead;                     // max steps wave w may run ahead of wave w+1 (<= ST_LEAD)
     // Z-slab mode (one GPU per slab of the grid).  Tiles cover oriented c in
@@ -115,6 +124,8 @@ struct StParams {
     int cs, ce;
     const unsigned long long *hc_in;
     unsigned long long *hc_out;
+    int seen[7];   // per upwind slot q: s'+1 of the last earlier sweep in which an interior cell
+                   // examined that neighbour (-1: none) -- see sweep_sparse.hpp
 };
 
 __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
@@ -122,16 +133,16 @@ __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
     return (size_t)(b + 1) * (size_t)(P.A + 1) + (size_t)(a + 1);
 }
 
-// label of a granule published for this sweep (bounded spin; error bit 4 on timeout)
-__device__ __forceinline__ int st_inbox_label(const StParams &P, const unsigned long long *p)
+// low word of a granule published for this sweep (bounded spin; error bit 4 on timeout)
+__device__ __forceinline__ uint32_t st_inbox_word(const StParams &P, const unsigned long long *p)
 {
     for (unsigned spins = 0;; ++spins) {
         const unsigned long long g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        if ((uint32_t)(g >> 32) == P.epoch) return (int)(uint32_t)g;
+        if (st_granule_ready(g, P.epoch)) return (uint32_t)g;
         if (spins > ST_WATCHDOG) {
             atomicOr(P.err, 4);
             atomicMax(P.err + 1, P.sweep + 1);
-            return -1;
+            return 0xffffffffu;
         }
         __builtin_amdgcn_s_sleep(4);
     }
@@ -160,12 +171,6 @@ __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v,
 // all of this wave's LDS writes have executed before anything after this point
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-#ifdef ST_DEBUG_TAGS
-// debug builds: the spare .w of an entry's third float4 carries (kind, column/stream, a+1)
-#define ST_TAGF(kind, id, a) __int_as_float(((kind) << 28) | ((id) << 16) | (((a) + 1) & 0xffff))
-#else
-#define ST_TAGF(kind, id, a) 0.f
-#endif
 
 __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v0, float4 &v1, float4 &v2)
 {
@@ -204,8 +209,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         const int nf = P.A + 1 + P.B;
         for (int f = blockIdx.x * ST_THREADS + tid; f < nf; f += gridDim.x * ST_THREADS) {
             const int a = f <= P.A ? f - 1 : -1, b = f <= P.A ? -1 : f - (P.A + 1);
-            const unsigned t = (uint32_t)P.cell[st_phys(P, a, b, P.ce - 1)];
-            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), ((unsigned long long)P.epoch << 32) | t,
+            const uint32_t w = (uint32_t)P.cell[st_phys(P, a, b, P.ce - 1)];
+            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), st_granule(P.epoch, w),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
@@ -227,13 +232,13 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 const int bl = L & (ST_T - 1), cl = ST_CLW * wave + (L >> 3);
                 const int b = b0 + bl, c = c0 + cl;
                 float4 v0, v1, v2;
-                int t = -1;
-                if (b < P.B && c < P.ce) t = (int)(uint32_t)P.cell[st_phys(P, -1, b, c)];
-                st_load_tri(P.soup, t, v0, v1, v2);
+                uint32_t w = 0xffffffffu;
+                if (b < P.B && c < P.ce) w = (uint32_t)P.cell[st_phys(P, -1, b, c)];
+                st_load_tri(P.soup, lbl_of(w), v0, v1, v2);
                 const int e = ST_RING0 + (ST_RR - 1) * ST_NCOL + cl * ST_T + bl;
-                s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
+                s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __uint_as_float(w));
                 s_ent[3 * e + 1] = v1;
-                s_ent[3 * e + 2] = make_float4(v2.x, v2.y, v2.z, ST_TAGF(1, cl * ST_T + bl, -1));
+                s_ent[3 * e + 2] = v2;
             }
             if (L == 0) s_prog[wave] = 0;
             if (wave == 0 && L == 0) {
@@ -247,16 +252,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             else if (L < 2 * ST_T) { hb_ = b0 + (L - ST_T); hc_ = c0 - 1; valid = hb_ < P.B; }
             else { hb_ = b0 - 1; hc_ = c0 - 1; valid = true; }
             float4 v0, v1, v2;
-            int t = -1;
+            uint32_t w = 0xffffffffu;
             if (valid) {
-                if (inbox && L >= ST_T) t = st_inbox_label(P, P.hc_in + st_inbox(P, -1, hb_));
-                else t = (int)(uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
+                if (inbox && L >= ST_T) w = st_inbox_word(P, P.hc_in + st_inbox(P, -1, hb_));
+                else w = (uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
             }
-            st_load_tri(P.soup, t, v0, v1, v2);
+            st_load_tri(P.soup, lbl_of(w), v0, v1, v2);
             const int e = ST_HALO0 + L * ST_RH + (ST_RH - 1);
-            s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __int_as_float(t));
+            s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __uint_as_float(w));
             s_ent[3 * e + 1] = v1;
-            s_ent[3 * e + 2] = make_float4(v2.x, v2.y, v2.z, ST_TAGF(3, L, -1));
+            s_ent[3 * e + 2] = v2;
             s_halo_ready[L] = valid ? 0 : P.A;
         }
         __syncthreads();
@@ -336,46 +341,33 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 // ---- candidates: the 7 upwind labels minus exact duplicates ----
                 float phi = 0.f;
                 int ct = -1, ct_orig = -1, win = -1;
+                uint32_t own_w = 0xffffffffu;
                 int lab[7], ent[7];
                 unsigned fmask = 0;
                 const int e_own = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id;
                 if (act) {
                     const float4 o0 = s_ent[3 * e_own], o1 = s_ent[3 * e_own + 1];
-                    ct = __float_as_int(o0.w);
+                    own_w = __float_as_uint(o0.w);
+                    ct = lbl_of(own_w);
                     phi = o1.w;
                     ct_orig = ct;
+                    int lcq[7];
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         const int aq = (q & 1) == 0 ? a - 1 : a;   // q = 0,2,4,6 read a-1
                         ent[q] = nb_base[q] + (aq & nb_mask[q]) * nb_stride[q];
-                        lab[q] = __float_as_int(s_ent[3 * ent[q]].w);
+                        const uint32_t wq = __float_as_uint(s_ent[3 * ent[q]].w);
+                        lab[q] = lbl_of(wq);
+                        lcq[q] = lc_of(wq);
                     }
-#ifdef ST_DEBUG_TAGS
-                    {
-                        const int og = __float_as_int(s_ent[3 * e_own + 2].w);
-                        const int oe = __float_as_int(ST_TAGF(2, col_id, a));
-                        if (og != oe && atomicAdd(P.err + 2, 1) < 24)
-                            printf("TAG own J=%d K=%d w=%d h=%d bl=%d cl=%d a=%d want %08x got %08x own_fill=%d prog=%d,%d,%d,%d\n",
-                                   J, K, w, h, bl, cl, a, oe, og, s_own_fill, s_prog[0], s_prog[ST_NCW > 1 ? 1 : 0],
-                                   s_prog[ST_NCW > 2 ? 2 : 0], s_prog[ST_NCW - 1]);
-                        for (int q = 0; q < 7; ++q) {
-                            const int aq = (q & 1) == 0 ? a - 1 : a;
-                            const bool isring = nb_stride[q] == ST_NCOL;
-                            const int id = isring ? nb_base[q] - ST_RING0 : (nb_base[q] - ST_HALO0) / ST_RH;
-                            const int want = __float_as_int(ST_TAGF(isring ? 1 : 3, id, aq));
-                            const int got = __float_as_int(s_ent[3 * ent[q] + 2].w);
-                            if (want != got && atomicAdd(P.err + 2, 1) < 24)
-                                printf("TAG nb J=%d K=%d w=%d h=%d bl=%d cl=%d a=%d q=%d want %08x got %08x prog=%d,%d,%d,%d hr=%d\n",
-                                       J, K, w, h, bl, cl, a, q, want, got, s_prog[0], s_prog[ST_NCW > 1 ? 1 : 0],
-                                       s_prog[ST_NCW > 2 ? 2 : 0], s_prog[ST_NCW - 1], isring ? -1 : s_halo_ready[id]);
-                        }
-                    }
-#endif
+                    // interior cells took part in every earlier sweep (sweep_sparse.hpp: exact skip)
+                    const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         bool skip = (lab[q] < 0) || (lab[q] == ct_orig);
 #pragma unroll
                         for (int r = 0; r < q; ++r) skip = skip || (lab[r] == lab[q]);
+                        skip = skip || (interior && lcq[q] <= P.seen[q]);   // seen[q] = -1: never
                         if (!skip) fmask |= 1u << q;
                     }
                 }
@@ -431,15 +423,13 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     const float4 w0 = s_ent[3 * src];
                     const float4 w1 = s_ent[3 * src + 1], w2 = s_ent[3 * src + 2];
                     const int slot = ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id;
-                    s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __int_as_float(ct));
+                    // a winner always carries a new label (the own label is never a candidate)
+                    const uint32_t w_new = win >= 0 ? lo_word(ct, P.sweep + 1) : own_w;
+                    s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
                     s_ent[3 * slot + 1] = w1;
-                    s_ent[3 * slot + 2] = make_float4(w2.x, w2.y, w2.z, ST_TAGF(1, col_id, a));
-                    if (win >= 0) {   // a winner always carries a new label (own label is never a candidate)
-                        const size_t ph = st_phys(P, a, b, c);
-                        P.cell[ph] = ((unsigned long long)__float_as_uint(phi) << 32) | (uint32_t)ct;
-                        if (P.lc) P.lc[ph] = (unsigned char)(P.sweep + 1);
-                    }
-                    const unsigned long long gran = ((unsigned long long)P.epoch << 32) | (uint32_t)ct;
+                    s_ent[3 * slot + 2] = w2;
+                    if (win >= 0) P.cell[st_phys(P, a, b, c)] = ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
+                    const unsigned long long gran = st_granule(P.epoch, w_new);
                     if (bl == ST_T - 1 && J < P.nJ - 1)
                         __hip_atomic_store(P.hb + ((size_t)J * P.C + c) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
                     if (cl == ST_T - 1 && K < P.nK - 1)
@@ -521,16 +511,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                              "+v"(q2), "+v"(q3)::"memory");
                 // ---- stage 2: vertices for batch A ----
                 int hp = 0;   // ready prefix of the halo batch (tag == epoch; boundary planes always)
-                const bool r0 = hbound || (uint32_t)(q0 >> 32) == P.epoch;
-                const bool r1 = hbound || (uint32_t)(q1 >> 32) == P.epoch;
-                const bool r2 = hbound || (uint32_t)(q2 >> 32) == P.epoch;
-                const bool r3 = hbound || (uint32_t)(q3 >> 32) == P.epoch;
+                const bool r0 = hbound || st_granule_ready(q0, P.epoch);
+                const bool r1 = hbound || st_granule_ready(q1, P.epoch);
+                const bool r2 = hbound || st_granule_ready(q2, P.epoch);
+                const bool r3 = hbound || st_granule_ready(q3, P.epoch);
                 if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
 #define ST_GATHER(g, cg, qg)                                                                          \
-    const size_t so##g = 3 * (size_t)(ST_OWN_OK(g) && (int)(uint32_t)(cg) >= 0 ? (uint32_t)(cg) : 0u); \
+    const size_t so##g = 3 * (size_t)(ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : 0); \
     const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
-    const size_t sh##g = 3 * (size_t)((g) < hp && (int)(uint32_t)(qg) >= 0 ? (uint32_t)(qg) : 0u);     \
+    const size_t sh##g = 3 * (size_t)((g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : 0); \
     const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
                 ST_GATHER(0, c0, q0)
                 ST_GATHER(1, c1, q1)
@@ -552,7 +542,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     {                                                                                                  \
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
-        cn = P.cell[ok_ ? st_phys(P, a_, b, c) : dummy];                                               \
+        const size_t ix_ = ok_ ? st_phys(P, a_, b, c) : dummy;                                         \
+        cn = P.cell[ix_];                                                                              \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + dummy : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g)); \
         qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE);                                        \
@@ -574,15 +565,15 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
 #define ST_LAND(g, cg, qg)                                                                             \
     if (ST_OWN_OK(g)) {                                                                                \
         const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + L;                   \
-        s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __int_as_float((int)(uint32_t)(cg)));   \
+        s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __uint_as_float((uint32_t)(cg)));      \
         s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
-        s_ent[3 * e_ + 2] = make_float4(oc##g.x, oc##g.y, oc##g.z, ST_TAGF(2, L, fA + (g) - bl - cl)); \
+        s_ent[3 * e_ + 2] = oc##g;                                                                     \
     }                                                                                                  \
     if ((g) < hp) {                                                                                    \
         const int e_ = ST_HALO0 + L * ST_RH + ((hA + (g)) & (ST_RH - 1));                              \
-        s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __int_as_float((int)(uint32_t)(qg)));   \
+        s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __uint_as_float((uint32_t)(qg)));      \
         s_ent[3 * e_ + 1] = hb##g;                                                                     \
-        s_ent[3 * e_ + 2] = make_float4(hc##g.x, hc##g.y, hc##g.z, ST_TAGF(3, L, hA + (g)));        \
+        s_ent[3 * e_ + 2] = hc##g;                                                                     \
     }
                 ST_LAND(0, c0, q0)
                 ST_LAND(1, c1, q1)
@@ -638,6 +629,7 @@ struct TileSweepWorkspace {
     int cur_sweep = 0;
     int grid_override = 0;     // diagnostics: cap on resident workgroups
     int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
+    bool skip_seen = true;     // the "already examined" skip (diagnostics can turn it off)
     size_t cap_hb = 0, cap_hc = 0;
     // task tables (dequeue order) for up to two tile grids: a Z-slab alternates between
     // two c extents (k-up and k-down sweeps), and a table must not be rewritten while a
@@ -676,7 +668,7 @@ struct TileSlab {
 
 // Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
-                      unsigned char *lc, const float origin[3], float dx, int ni, int nj, int nk, int di, int dj,
+                      const float origin[3], float dx, int ni, int nj, int nk, int di, int dj,
                       int dk, char *err, size_t errlen, const TileSlab &slab = TileSlab())
 {
     const int A = ni - 1, B = nj - 1, C = nk - 1;
@@ -721,7 +713,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
         W.task_nJ[ti] = nJ;
         W.task_nK[ti] = nK;
     }
-    if (++W.epoch == 0) ++W.epoch;
+    if (++W.epoch == 0) ++W.epoch;   // 0 = never published
     if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     StParams P;
     P.soup = soup;
@@ -754,8 +746,20 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.dj = dj;
     P.dk = dk;
     P.epoch = W.epoch;
-    P.lc = lc;
     P.sweep = W.cur_sweep;
+    for (int q = 0; q < 7; ++q) {   // same table as sweep_sparse.hpp
+        const int m = q + 1;
+        P.seen[q] = -1;
+        for (int s2 = W.cur_sweep - 1; s2 >= 0 && W.skip_seen; --s2) {
+            static const int D[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
+                                        {+1, -1, +1}, {-1, +1, -1}, {+1, -1, -1}, {-1, +1, +1}};
+            const int *d = D[s2 % 8];
+            if ((!(m & 1) || d[0] == di) && (!(m & 2) || d[1] == dj) && (!(m & 4) || d[2] == dk)) {
+                P.seen[q] = s2 + 1;
+                break;
+            }
+        }
+    }
     P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
     P.cs = cs;
     P.ce = ce;

@@ -1,2 +1,5 @@
 set -e
-for v in v1 v2 v3 v4 v5 v6; do echo $v; SDFGEN_OCC=1 SDFGEN_LIB_OVERRIDE=sdfgen_amd/build_var/$v/libsdfgen_hip.so timeout -k 10 200 python tools/trace_diag.py c3_sphere1m_256 3 2>&1 | grep -E "occupancy|active|sweep 3" | sort | uniq ; SDFGEN_LIB_OVERRIDE=sdfgen_amd/build_var/$v/libsdfgen_hip.so timeout -k 10 200 python tools/race_diag.py 16; SDFGEN_LIB_OVERRIDE=sdfgen_amd/build_var/$v/libsdfgen_hip.so timeout -k 10 200 python tools/sweep_times.py | tail -1; done
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_sp.log 2>&1 || (tail -40 gpurun_out/pytest_sp.log; exit 1)
+tail -2 gpurun_out/pytest_sp.log
+timeout -k 10 120 python tools/sweep_times.py
+SDFGEN_NO_SEEN_SKIP=1 timeout -k 10 120 python tools/sweep_times.py
