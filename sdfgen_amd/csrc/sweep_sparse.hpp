@@ -194,8 +194,16 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
 // Pass 1 of the sparse sweep: every cell against the labels of S.
 __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 {
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    for (unsigned long long c = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; c < P.n; c += stride) {
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so XCD x walks the x-th
+    // contiguous eighth of the grid -- the neighbour planes a cell reads sit in its own L2.
+    const bool xcd = gridDim.x % 8 == 0;
+    const unsigned long long span = xcd ? (P.n + 7) / 8 : P.n;
+    const unsigned long long base = xcd ? (unsigned long long)(blockIdx.x % 8) * span : 0ull;
+    const unsigned long long first = (unsigned long long)(xcd ? blockIdx.x / 8 : blockIdx.x) * blockDim.x + threadIdx.x;
+    const unsigned long long step = (unsigned long long)(xcd ? gridDim.x / 8 : gridDim.x) * blockDim.x;
+    for (unsigned long long it = first; it < span; it += step) {
+        const unsigned long long c = base + it;
+        if (c >= P.n) break;
         const unsigned c32 = (unsigned)c;   // n < 2^32 (sparse_sweep_supported)
         const int i = (int)(c32 % (unsigned)P.ni);
         const unsigned r = c32 / (unsigned)P.ni;
@@ -367,6 +375,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     }
     unsigned long long blocks = (n + 255) / 256;
     if (blocks > 16384) blocks = 16384;
+    blocks = (blocks + 7) / 8 * 8;   // a multiple of the 8 XCDs (k_sp_jacobi's traversal)
     hipLaunchKernelGGL(k_sp_jacobi, dim3((unsigned)blocks), dim3(256), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
     hipLaunchKernelGGL(k_sp_recheck, dim3(nw), dim3(64), 0, st, P);

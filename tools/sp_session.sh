@@ -1,5 +1,5 @@
 set -e
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_sp.log 2>&1 || (tail -40 gpurun_out/pytest_sp.log; exit 1)
-tail -2 gpurun_out/pytest_sp.log
-timeout -k 10 120 python tools/sweep_times.py
-SDFGEN_NO_SEEN_SKIP=1 timeout -k 10 120 python tools/sweep_times.py
+export TMPDIR=/tmp
+rm -rf gpurun_out/prof_sp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sp -o run -- python tools/sweep_times.py > /dev/null 2>&1
+cut -c1-120 gpurun_out/prof_sp/run_kernel_stats.csv | head -8
