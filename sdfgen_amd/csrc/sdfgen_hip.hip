@@ -4,9 +4,10 @@
 // Pipeline (one HIP stream per call):
 //   k_prep   : gather the indexed mesh into a per-triangle vertex soup (48 B/tri),
 //              validate indices, initialise the cell state         (:196-199)
-//   k_band   : one wave per triangle -- exact distances over the band box with a
-//              packed u64 atomicMin key (f32bits(d)<<32 | t) that reproduces the
-//              CPU's ascending-t strict-< rule, and ray-parity counts (:203-236)
+//   k_band_lds: batches of 32 consecutive triangles per workgroup -- exact distances over
+//              the band boxes, merged per cell in LDS, then one global atomicMin on the
+//              packed u64 key (f32bits(d)<<32 | t) that reproduces the CPU's
+//              ascending-t strict-< rule; ray-parity counts (:203-236)
 //   sweeps   : 2 passes x 8 directions of the Gauss-Seidel sweep (:238-292),
 //              reproduced bit-exactly by a hyperplane-ordered wavefront
 //   k_sign   : one wave per (j,k) row -- ballot prefix parity, sign flip, output in
@@ -16,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -109,76 +111,145 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
     return (size_t)i + (size_t)ni * ((size_t)j + (size_t)nj * (size_t)k);
 }
 
-// Narrow band + ray parity, one 64-lane wave per triangle (grid-stride over triangles).
-//   :206-220 band, :222-235 parity
-// [k_lo, k_hi): the k planes this call owns (a Z-slab; 0..nk for the whole grid).  Boxes are
-// clamped to the whole grid first (:210-212), then cut to the slab, so every slab sees
-// exactly the reference's cells.
-__global__ void __launch_bounds__(256) k_band(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
-                                              float init, u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
-                                              unsigned long long *__restrict__ eval_count, int k_lo, int k_hi)
+// Band + ray parity for batches of BT consecutive triangles per workgroup (:203-236).
+// Consecutive triangles of a mesh are usually neighbours, so their band boxes overlap:
+// the batch's candidates are first merged per cell in LDS (ds_min_u64 on the same
+// (f32bits(d) << 32 | t) keys), and only the union box's winners go to HBM with one
+// global atomicMin each -- about 5x fewer global atomics than one per (triangle, cell).
+// A batch whose union box does not fit the LDS table falls back to direct global
+// atomics.  min() is order-independent, so the result is the one-triangle-at-a-time
+// result bit for bit.
+constexpr int BAND_BT = 32;             // triangles per batch
+constexpr int BAND_LDS = 5120;          // u64 keys in the LDS table (40 KB)
+
+struct BandBox {
+    int i0, j0, k0, bi, bj, bk;         // clamped band box (bi*bj*bk cells; 0 = empty)
+};
+
+__device__ __forceinline__ void band_box(const float4 *soup, uint64_t t, const Grid &g, int band, int k_lo, int k_hi,
+                                         BandBox &B, double f[9])
 {
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const f3 xp = load_vtx(soup, t, 0), xq = load_vtx(soup, t, 1), xr = load_vtx(soup, t, 2);
+    const double ox = g.ox, oy = g.oy, oz = g.oz, ddx = g.dx;
+    f[0] = ((double)xp.x - ox) / ddx; f[1] = ((double)xp.y - oy) / ddx; f[2] = ((double)xp.z - oz) / ddx;
+    f[3] = ((double)xq.x - ox) / ddx; f[4] = ((double)xq.y - oy) / ddx; f[5] = ((double)xq.z - oz) / ddx;
+    f[6] = ((double)xr.x - ox) / ddx; f[7] = ((double)xr.y - oy) / ddx; f[8] = ((double)xr.z - oz) / ddx;
+    const int i0 = clampi(wrap_add(trunc_to_int(dmin3(f[0], f[3], f[6])), -band), 0, g.ni - 1);
+    const int i1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(f[0], f[3], f[6])), band), 1), 0, g.ni - 1);
+    const int j0 = clampi(wrap_add(trunc_to_int(dmin3(f[1], f[4], f[7])), -band), 0, g.nj - 1);
+    const int j1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(f[1], f[4], f[7])), band), 1), 0, g.nj - 1);
+    int k0 = clampi(wrap_add(trunc_to_int(dmin3(f[2], f[5], f[8])), -band), 0, g.nk - 1);
+    int k1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(f[2], f[5], f[8])), band), 1), 0, g.nk - 1);
+    k0 = max(k0, k_lo);
+    k1 = min(k1, k_hi - 1);
+    B.i0 = i0;
+    B.j0 = j0;
+    B.k0 = k0;
+    const bool ok = i1 >= i0 && j1 >= j0 && k1 >= k0;
+    B.bi = ok ? i1 - i0 + 1 : 0;
+    B.bj = ok ? j1 - j0 + 1 : 0;
+    B.bk = ok ? k1 - k0 + 1 : 0;
+}
+
+__global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
+                                                  float init, u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
+                                                  unsigned long long *__restrict__ eval_count, int k_lo, int k_hi)
+{
+    __shared__ u64 s_key[BAND_LDS];
+    __shared__ BandBox s_box[BAND_BT];
+    __shared__ unsigned s_pre[BAND_BT + 1];   // prefix sums of the box volumes
+    __shared__ int s_u[6];                    // union box: i0, j0, k0, ni, nj, nk
+    const int tid = threadIdx.x;
     unsigned long long evals = 0;
-    for (uint64_t t = wave; t < ntri; t += nwaves) {
-        f3 xp = load_vtx(soup, t, 0), xq = load_vtx(soup, t, 1), xr = load_vtx(soup, t, 2);
-        const double ox = g.ox, oy = g.oy, oz = g.oz, ddx = g.dx;
-        double fip = ((double)xp.x - ox) / ddx, fjp = ((double)xp.y - oy) / ddx, fkp = ((double)xp.z - oz) / ddx;
-        double fiq = ((double)xq.x - ox) / ddx, fjq = ((double)xq.y - oy) / ddx, fkq = ((double)xq.z - oz) / ddx;
-        double fir = ((double)xr.x - ox) / ddx, fjr = ((double)xr.y - oy) / ddx, fkr = ((double)xr.z - oz) / ddx;
-        int i0 = clampi(wrap_add(trunc_to_int(dmin3(fip, fiq, fir)), -band), 0, g.ni - 1);
-        int i1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fip, fiq, fir)), band), 1), 0, g.ni - 1);
-        int j0 = clampi(wrap_add(trunc_to_int(dmin3(fjp, fjq, fjr)), -band), 0, g.nj - 1);
-        int j1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fjp, fjq, fjr)), band), 1), 0, g.nj - 1);
-        int k0 = clampi(wrap_add(trunc_to_int(dmin3(fkp, fkq, fkr)), -band), 0, g.nk - 1);
-        int k1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fkp, fkq, fkr)), band), 1), 0, g.nk - 1);
-        k0 = max(k0, k_lo);
-        k1 = min(k1, k_hi - 1);
-        if (i1 >= i0 && j1 >= j0 && k1 >= k0) {
-            const uint32_t bi = (uint32_t)(i1 - i0 + 1), bj = (uint32_t)(j1 - j0 + 1);
-            const uint64_t bij = (uint64_t)bi * bj;
-            const uint64_t total = bij * (uint64_t)(k1 - k0 + 1);
-            evals += total;
-            for (uint64_t c = lane; c < total; c += 64) {
-                const uint32_t kk = (uint32_t)(c / bij);
-                const uint32_t rem = (uint32_t)(c - (uint64_t)kk * bij);
-                const uint32_t jj = rem / bi;
-                const int i = i0 + (int)(rem - jj * bi), j = j0 + (int)jj, k = k0 + (int)kk;
-                f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
-                float d = ptd(gx, xp, xq, xr);
-                if (d < init) {  // also rejects NaN
-                    u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * BAND_BT; t0 < ntri; t0 += (uint64_t)gridDim.x * BAND_BT) {
+        const int nb = (int)min<uint64_t>(BAND_BT, ntri - t0);
+        double f[9];
+        if (tid < BAND_BT) {
+            BandBox B{0, 0, 0, 0, 0, 0};
+            if (tid < nb) band_box(soup, t0 + tid, g, band, k_lo, k_hi, B, f);
+            s_box[tid] = B;
+            // ray-parity lattice of this triangle (:222-235), one thread per triangle
+            if (tid < nb) {
+                int pj0 = clampi(trunc_to_int(ceil(dmin3(f[1], f[4], f[7]))), 0, g.nj - 1);
+                int pj1 = clampi(trunc_to_int(floor(dmax3(f[1], f[4], f[7]))), 0, g.nj - 1);
+                int pk0 = clampi(trunc_to_int(ceil(dmin3(f[2], f[5], f[8]))), 0, g.nk - 1);
+                int pk1 = clampi(trunc_to_int(floor(dmax3(f[2], f[5], f[8]))), 0, g.nk - 1);
+                pk0 = max(pk0, k_lo);
+                pk1 = min(pk1, k_hi - 1);
+                for (int k = pk0; k <= pk1; ++k)
+                    for (int j = pj0; j <= pj1; ++j) {
+                        double a, b, cc;
+                        if (pit2d((double)j, (double)k, f[1], f[2], f[4], f[5], f[7], f[8], a, b, cc)) {
+                            const double fi = (a * f[0] + b * f[3]) + cc * f[6];
+                            const int ii = trunc_to_int(ceil(fi));
+                            if (ii < 0) atomicAdd(cnt + cidx(0, j, k, g.ni, g.nj), 1u);
+                            else if (ii < g.ni) atomicAdd(cnt + cidx(ii, j, k, g.ni, g.nj), 1u);
+                        }
+                    }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            unsigned acc = 0;
+            int ui0 = INT_MAX, uj0 = INT_MAX, uk0 = INT_MAX, ui1 = -1, uj1 = -1, uk1 = -1;
+            for (int q = 0; q < nb; ++q) {
+                const BandBox B = s_box[q];
+                s_pre[q] = acc;
+                acc += (unsigned)(B.bi * B.bj * B.bk);
+                if (B.bi) {
+                    ui0 = min(ui0, B.i0); uj0 = min(uj0, B.j0); uk0 = min(uk0, B.k0);
+                    ui1 = max(ui1, B.i0 + B.bi - 1); uj1 = max(uj1, B.j0 + B.bj - 1); uk1 = max(uk1, B.k0 + B.bk - 1);
+                }
+            }
+            s_pre[nb] = acc;
+            s_u[0] = ui0; s_u[1] = uj0; s_u[2] = uk0;
+            s_u[3] = ui1 >= ui0 ? ui1 - ui0 + 1 : 0;
+            s_u[4] = uj1 >= uj0 ? uj1 - uj0 + 1 : 0;
+            s_u[5] = uk1 >= uk0 ? uk1 - uk0 + 1 : 0;
+        }
+        __syncthreads();
+        const unsigned total = s_pre[nb];
+        evals += tid == 0 ? total : 0;
+        const int ui0 = s_u[0], uj0 = s_u[1], uk0 = s_u[2], uni = s_u[3], unj = s_u[4];
+        const unsigned long long uvol = (unsigned long long)uni * unj * (unsigned)s_u[5];
+        const bool merge = uvol > 0 && uvol <= BAND_LDS;
+        if (merge)
+            for (unsigned c = tid; c < uvol; c += 256) s_key[c] = ~0ull;
+        __syncthreads();
+        for (unsigned fl = tid; fl < total; fl += 256) {
+            int q = 0;   // triangle of flat index fl: last q with s_pre[q] <= fl
+#pragma unroll
+            for (int step = BAND_BT / 2; step >= 1; step >>= 1)
+                if (q + step < nb && s_pre[q + step] <= fl) q += step;
+            const BandBox B = s_box[q];
+            const unsigned r = fl - s_pre[q], bij = (unsigned)(B.bi * B.bj);
+            const unsigned kk = r / bij, rem = r - kk * bij, jj = rem / (unsigned)B.bi;
+            const int i = B.i0 + (int)(rem - jj * (unsigned)B.bi), j = B.j0 + (int)jj, k = B.k0 + (int)kk;
+            const uint64_t t = t0 + q;
+            const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
+            const float d = ptd(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2));
+            if (d < init) {   // also rejects NaN
+                const u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
+                if (merge) {
+                    atomicMin(&s_key[(unsigned)((k - uk0) * unj + (j - uj0)) * (unsigned)uni + (unsigned)(i - ui0)], key);
+                } else {
                     u64 *p = cell + cidx(i, j, k, g.ni, g.nj);
                     if (key < *p) atomicMin(p, key);
                 }
             }
         }
-        // ray-parity counts
-        int pj0 = clampi(trunc_to_int(ceil(dmin3(fjp, fjq, fjr))), 0, g.nj - 1);
-        int pj1 = clampi(trunc_to_int(floor(dmax3(fjp, fjq, fjr))), 0, g.nj - 1);
-        int pk0 = clampi(trunc_to_int(ceil(dmin3(fkp, fkq, fkr))), 0, g.nk - 1);
-        int pk1 = clampi(trunc_to_int(floor(dmax3(fkp, fkq, fkr))), 0, g.nk - 1);
-        pk0 = max(pk0, k_lo);
-        pk1 = min(pk1, k_hi - 1);
-        if (pj1 >= pj0 && pk1 >= pk0) {
-            const uint32_t bj = (uint32_t)(pj1 - pj0 + 1);
-            const uint64_t total = (uint64_t)bj * (uint64_t)(pk1 - pk0 + 1);
-            for (uint64_t c = lane; c < total; c += 64) {
-                const uint32_t kk = (uint32_t)(c / bj);
-                const int j = pj0 + (int)(c - (uint64_t)kk * bj), k = pk0 + (int)kk;
-                double a, b, cc;
-                if (pit2d((double)j, (double)k, fjp, fkp, fjq, fkq, fjr, fkr, a, b, cc)) {
-                    double fi = (a * fip + b * fiq) + cc * fir;
-                    int ii = trunc_to_int(ceil(fi));
-                    if (ii < 0) atomicAdd(cnt + cidx(0, j, k, g.ni, g.nj), 1u);
-                    else if (ii < g.ni) atomicAdd(cnt + cidx(ii, j, k, g.ni, g.nj), 1u);
-                }
+        __syncthreads();
+        if (merge)
+            for (unsigned c = tid; c < uvol; c += 256) {
+                const u64 key = s_key[c];
+                if (key == ~0ull) continue;
+                const unsigned ij = (unsigned)(uni * unj), kk = c / ij, rem = c - kk * ij, jj = rem / (unsigned)uni;
+                u64 *p = cell + cidx(ui0 + (int)(rem - jj * (unsigned)uni), uj0 + (int)jj, uk0 + (int)kk, g.ni, g.nj);
+                if (key < *p) atomicMin(p, key);
             }
-        }
+        __syncthreads();
     }
-    if (eval_count && lane == 0 && evals) atomicAdd(eval_count, evals);
+    if (eval_count && tid == 0 && evals) atomicAdd(eval_count, evals);
 }
 
 // One sweep cell update: the CPU's sequential check_neighbour chain (:90-102, :143-149)
@@ -411,7 +482,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev[1], st));
     if (ntri) {
-        hipLaunchKernelGGL(k_band, dim3(grid_for(ntri * 64, 256, 65536)), dim3(256), 0, st, ws->soup, ntri, g, band,
+        hipLaunchKernelGGL(k_band_lds, dim3(grid_for((ntri + BAND_BT - 1) / BAND_BT, 1, 8192)), dim3(256), 0, st, ws->soup, ntri, g, band,
                            init, ws->cell, ws->cnt, ws->evals, 0, nk);
         HIPCHK(hipGetLastError());
     }
@@ -673,7 +744,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev[1], st));
     if (ntri) {
-        hipLaunchKernelGGL(k_band, dim3(grid_for(ntri * 64, 256, 65536)), dim3(256), 0, st, S->soup, ntri, g, band,
+        hipLaunchKernelGGL(k_band_lds, dim3(grid_for((ntri + BAND_BT - 1) / BAND_BT, 1, 8192)), dim3(256), 0, st, S->soup, ntri, g, band,
                            init, S->cell, S->cnt, S->evals, S->k_begin, S->k_end);
         HIPCHK(hipGetLastError());
     }

@@ -1,5 +1,4 @@
 set -e
-export TMPDIR=/tmp
-rm -rf gpurun_out/prof_sp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sp -o run -- python tools/sweep_times.py > /dev/null 2>&1
-cut -c1-120 gpurun_out/prof_sp/run_kernel_stats.csv | head -8
+timeout -k 10 600 python -m pytest tests -m gpu -x -q 2>&1 | tail -2
+timeout -k 10 120 python tools/sweep_times.py
+timeout -k 10 300 python bench.py --workload c4_sphere1m_512 --steps 1 --warmup 1 --no-cpu-baseline | cut -c1-200
