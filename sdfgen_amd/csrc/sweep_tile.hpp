@@ -185,7 +185,8 @@ __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v
 
 // SLAB: halo granules may come from another GPU (IPC-mapped inbox), so granule loads
 // and stores are made at system scope; the single-GPU build keeps agent scope.
-template <bool SLAB>
+// TRACE: per-task timestamps for tools/trace_diag.py (kept out of the normal build's loop).
+template <bool SLAB, bool TRACE>
 __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams P)
 {
     constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
@@ -266,7 +267,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         }
         __syncthreads();
 
-        if (P.trace && tid == 0) P.trace[8 * task] = wall_clock64();
+        if (TRACE && P.trace && tid == 0) P.trace[8 * task] = wall_clock64();
         if (wave < ST_NCW) {
             // ======================= compute waves =======================
             // Wave w owns the 16 columns cl in {2w, 2w+1}; lanes 0..15 are cells, all 64 lanes
@@ -319,7 +320,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         if (bl == 0 && cl == 0 && lds_ld(&s_halo_ready[2 * ST_T]) <= a) ok = false;
                     }
                     if (__all(ok)) break;
-                    if (P.trace && tw0 == 0) {
+                    if (TRACE && P.trace && tw0 == 0) {
                         tw0 = wall_clock64();
                         if (!__all(own_ok)) ++w_own; else ++w_halo;
                     }
@@ -333,10 +334,10 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     __builtin_amdgcn_s_sleep(1);
                 }
                 asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
-                if (tw0) t_wait += wall_clock64() - tw0;
+                if (TRACE && tw0) t_wait += wall_clock64() - tw0;
                 if (h >= nsteps) break;
-                const unsigned long long tc0 = P.trace ? wall_clock64() : 0ull;
-                const unsigned long long cc0 = P.trace ? clock64() : 0ull;
+                const unsigned long long tc0 = (TRACE && P.trace) ? wall_clock64() : 0ull;
+                const unsigned long long cc0 = (TRACE && P.trace) ? clock64() : 0ull;
                 polls = 0;
                 // ---- candidates: the 7 upwind labels minus exact duplicates ----
                 float phi = 0.f;
@@ -438,17 +439,17 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);
                 }
-                if (P.trace) {
+                if (TRACE && P.trace) {
                     t_comp += wall_clock64() - tc0;
                     c_comp += clock64() - cc0;
                 }
                 lds_drain();
                 if (L == 0) lds_st(&s_prog[w], h + 1);
-                if (P.trace && w == 0 && L == 0 && (h == 0 || h == nsteps / 2))
+                if (TRACE && P.trace && w == 0 && L == 0 && (h == 0 || h == nsteps / 2))
                     P.trace[8 * task + (h == 0 ? 1 : 2)] = wall_clock64();
             }
             __builtin_amdgcn_s_setprio(0);
-            if (P.trace && w == 0 && L == 0) {
+            if (TRACE && P.trace && w == 0 && L == 0) {
                 P.trace[8 * task + 3] = wall_clock64();
                 P.trace[8 * task + 4] = t_wait;
                 P.trace[8 * task + 5] = w_own + (w_halo << 32);
@@ -770,14 +771,15 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
     if (getenv("SDFGEN_OCC")) {   // diagnostics: resident workgroups per CU
         int occ = -1;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sweep_tile<false>, ST_THREADS, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sweep_tile<false, false>, ST_THREADS, 0);
         hipFuncAttributes fa;
-        (void)hipFuncGetAttributes(&fa, (const void *)k_sweep_tile<false>);
+        (void)hipFuncGetAttributes(&fa, (const void *)k_sweep_tile<false, false>);
         fprintf(stderr, "k_sweep_tile: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", occ, fa.numRegs,
                 fa.sharedSizeBytes, fa.localSizeBytes);
     }
-    if (slab.on) hipLaunchKernelGGL(k_sweep_tile<true>, dim3(grid), dim3(ST_THREADS), 0, st, P);
-    else hipLaunchKernelGGL(k_sweep_tile<false>, dim3(grid), dim3(ST_THREADS), 0, st, P);
+    if (slab.on) hipLaunchKernelGGL((k_sweep_tile<true, false>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    else if (P.trace) hipLaunchKernelGGL((k_sweep_tile<false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    else hipLaunchKernelGGL((k_sweep_tile<false, false>), dim3(grid), dim3(ST_THREADS), 0, st, P);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }
