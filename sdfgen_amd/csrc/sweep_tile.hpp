@@ -331,7 +331,10 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         h = nsteps;
                         break;
                     }
-                    __builtin_amdgcn_s_sleep(1);
+                    // waiting tiles back off: their polls share the SIMD with the tiles they wait for
+                    if (polls < 8) __builtin_amdgcn_s_sleep(1);
+                    else if (polls < 64) __builtin_amdgcn_s_sleep(2);
+                    else __builtin_amdgcn_s_sleep(8);
                 }
                 asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
                 if (TRACE && tw0) t_wait += wall_clock64() - tw0;
@@ -372,6 +375,28 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         if (!skip) fmask |= 1u << q;
                     }
                 }
+                // ---- at most one candidate per cell (the common case away from the surface):
+                //      each cell lane evaluates its own, no compaction and no LDS exchange ----
+                const bool single = __all(__popc(fmask) <= 1);
+                if (single) {
+                    if (fmask) {
+                        int e1 = ent[0], t1 = lab[0];
+#pragma unroll
+                        for (int q = 1; q < 7; ++q)
+                            if (fmask == (1u << q)) {   // static indices: no register-array indexing
+                                e1 = ent[q];
+                                t1 = lab[q];
+                            }
+                        const float d = ptd_nb(st_gx(P, a, b, c), st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]),
+                                               st_xyz(s_ent[3 * e1 + 2]));
+                        if (d < phi) {
+                            phi = d;
+                            ct = t1;
+                            win = e1;
+                        }
+                    }
+                    n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(fmask != 0)) : 0ull;
+                } else {
                 // ---- compact (cell, candidate) pairs across the wave ----
                 int total = 0;
 #pragma unroll
@@ -420,6 +445,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                             }
                         }
                     }
+                }
+                }
+                if (act) {
                     const int src = win < 0 ? e_own : win;
                     const float4 w0 = s_ent[3 * src];
                     const float4 w1 = s_ent[3 * src + 1], w2 = s_ent[3 * src + 2];
@@ -505,6 +533,30 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
 #pragma unroll
                 for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_prog[w]));
                 if (lds_ld(&s_abort)) break;
+                if (idle && gA == 0 && hcA == 0) {
+                    // Nothing in flight and the last round found nothing to do: wait cheaply (LDS
+                    // progress, at most one granule probe per halo lane) instead of running the
+                    // whole pipeline body on dummy loads -- idle helpers steal VALU issue slots
+                    // from the compute waves sharing their SIMD.
+                    if (__all(fA >= nsteps && hA >= P.A)) break;
+                    const int own_n = min(ST_G, min(nsteps - fA, prog + ST_RO - fA));
+                    const int halo_n = hvalid ? min(ST_G, min(P.A - hA, prog + ST_RH - hoff - 2 - hA)) : 0;
+                    bool go = own_n > 0;
+                    if (halo_n > 0)
+                        go = go || hbound ||
+                             st_granule_ready(__hip_atomic_load(hsrc + hA, __ATOMIC_RELAXED, GSCOPE), P.epoch);
+                    if (!__any(go)) {
+                        ++n_hpoll;
+                        if (++idle > ST_WATCHDOG) {
+                            if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
+                            break;
+                        }
+                        if (idle < 4) __builtin_amdgcn_s_sleep(1);
+                        else if (idle < 16) __builtin_amdgcn_s_sleep(4);
+                        else __builtin_amdgcn_s_sleep(16);
+                        continue;
+                    }
+                }
                 // The batch-A loads were issued one iteration ago: wait for them once, and hand
                 // the registers back through the asm so the compiler does not track them as
                 // pending (its per-use waits would otherwise serialise the gathers below).

@@ -1,4 +1,4 @@
 set -e
-timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -x -q -k "sweep_impls or golden" 2>&1 | tail -2
+timeout -k 10 600 python -m pytest tests -m gpu -x -q 2>&1 | tail -2
 timeout -k 10 120 python tools/sweep_times.py
-timeout -k 10 200 python tools/trace_diag.py c3_sphere1m_256 1 | tail -2
+SDFGEN_COUNT_EVALS=1 SDFGEN_SPARSE_FROM=16 timeout -k 10 120 python tools/sweep_times.py | tail -1
