@@ -262,15 +262,17 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             const unsigned long long cur = sp_ld64(P.X + e);
             const unsigned long long y = sp_eval<true>(P, P.X, i, j, k, e, P.S[e]);
             ++runs;
+            const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
             if (y != cur) {
                 sp_st64(P.X + e, y);
-                if (lbl_of((uint32_t)y) != lbl_of((uint32_t)cur)) {
-                    sp_order();   // the new label is visible before anyone is asked to read it
-                    const size_t m = sp_request_downstream(P, i, j, k, e, next == NONE);
-                    if (m != NONE) next = m;
-                }
+                if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
             }
+            // retire e's requests and ask for the downstream rechecks in one round trip
             const unsigned old = atomicSub(P.req + e, rq);
+            if (relabel) {
+                const size_t m = sp_request_downstream(P, i, j, k, e, next == NONE);
+                if (m != NONE) next = m;
+            }
             if (old == rq) {   // no request arrived meanwhile: e is settled
                 if (next != NONE) {
                     e = next;   // the work item's pending count carries over to the claimed cell
