@@ -6,7 +6,7 @@ One step = one complete make_level_set3 (prep, band + ray parity, 16 sweeps,
 sign) on the deterministic 1M-triangle bumpy sphere with inputs already
 resident in HBM and phi written to HBM (sdfgen_hip_make_level_set3_device).
 For N > 1 (launched by torch.distributed.run, one rank per GPU) the same grid is
-split into N Z-slabs (sdfgen_amd/distributed.py): each rank owns nk/N planes and the
+split into N Z-slabs (sdfgenfast_amd/distributed.py): each rank owns nk/N planes and the
 sweeps' wavefront runs across the GPUs (strong scaling); see DESIGN.md §7.
 
 Rank 0 prints one JSON line with the driver's contract fields plus
@@ -39,7 +39,7 @@ def cpu_baseline(workload: str):
     """Oracle (oracle/sdf_oracle.c, 1 thread) on a bounded sample: the same 1M-triangle
     mesh on a 128^3 grid (same mode-2b recipe) -- about 15 s of CPU work."""
     from oracle import oracle as O
-    from sdfgen_amd import meshgen
+    from sdfgenfast_amd import meshgen
 
     w = meshgen.WORKLOADS[workload]
     v, t = meshgen.bumpy_sphere(w["nu"], w["nv"])
@@ -71,14 +71,14 @@ def main():
     if world > 1:
         # Control plane (IPC-handle exchange, barriers, max of the wall time): gloo on the
         # host.  The data path is the slab wavefront itself: boundary planes move GPU to GPU
-        # inside the sweep kernels (sdfgen_amd/distributed.py).
+        # inside the sweep kernels (sdfgenfast_amd/distributed.py).
         # torch is imported BEFORE the backend so one HIP runtime serves both.
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")
 
-    from sdfgen_amd import _hiprt, _lib, meshgen
+    from sdfgenfast_amd import _hiprt, _lib, meshgen
 
     dev = local_rank % max(_lib.device_count(), 1)   # = local_rank on a node with a GPU per rank
     _hiprt.set_device(dev)
@@ -88,7 +88,7 @@ def main():
     dv = _hiprt.DeviceBuffer.from_array(v)
     dt = _hiprt.DeviceBuffer.from_array(t)
     if world > 1:
-        from sdfgen_amd import distributed as D
+        from sdfgenfast_amd import distributed as D
         sess = D._gpu_session(dist, None, dev, dims, world, rank)
         nks = sess.k_end - sess.k_begin
         out = _hiprt.DeviceBuffer(ni * nj * nks * 4)
@@ -175,7 +175,7 @@ def main():
             "scaling": "strong" if world > 1 else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (deterministic 1M-triangle bumpy UV-sphere, sdfgen_amd/meshgen.py)",
+            "data": "synthetic (deterministic 1M-triangle bumpy UV-sphere, sdfgenfast_amd/meshgen.py)",
             "config": {"workload": args.workload, "grid": list(dims), "triangles": int(t.shape[0]),
                        "exact_band": 1, "parallelism": f"zslab{world}" if world > 1 else "single-gpu",
                        "inputs": "HBM-resident"},

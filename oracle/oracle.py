@@ -1,7 +1,7 @@
 """ctypes front-end for the CPU parity checkers.  TEST INFRASTRUCTURE ONLY.
 
 Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
-this module.  The product package (sdfgen_amd) never does.
+this module.  The product package (sdfgenfast_amd) never does.
 
 * ``liboracle.so``  -- oracle/sdf_oracle.c, the C restatement of
   cpu_lib/makelevelset3.cpp:192-304 (single-thread semantics).

@@ -4,7 +4,7 @@
  * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
  * product path.  Only tests/, __graft_entry__.smoke() and bench.py's
  * cpu_baseline leg may load it (via oracle/oracle.py).  The product library
- * (sdfgen_amd/csrc) never links, loads or calls anything in oracle/.
+ * (sdfgenfast_amd/csrc) never links, loads or calls anything in oracle/.
  *
  * It restates, in plain C99, the single-threaded semantics of
  *   /root/reference/cpu_lib/makelevelset3.cpp:192-304  (sdfgen::cpu::make_level_set3,

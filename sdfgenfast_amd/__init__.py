@@ -1,4 +1,4 @@
-"""sdfgen_amd -- MI355X-native signed distance fields, drop-in for ``sdfgen``.
+"""sdfgenfast_amd -- MI355X-native signed distance fields, drop-in for ``sdfgen``.
 
 Mirrors the reference Python surface (sdfgen/__init__.py:29-279 and the
 nanobind module python/sdfgen_py.cpp:316-411):

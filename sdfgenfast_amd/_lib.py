@@ -84,7 +84,7 @@ def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build the HIP backend first "
-            "(python -c 'import __graft_entry__ as g; g.build()' or make -C sdfgen_amd)")
+            "(python -c 'import __graft_entry__ as g; g.build()' or make -C sdfgenfast_amd)")
     L = ctypes.CDLL(LIB_PATH)
     L.sdfgen_hip_abi_version.restype = ctypes.c_int
     L.sdfgen_hip_device_count.restype = ctypes.c_int

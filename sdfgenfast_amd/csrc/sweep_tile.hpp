@@ -133,13 +133,21 @@ __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
     return (size_t)(b + 1) * (size_t)(P.A + 1) + (size_t)(a + 1);
 }
 
+// A watchdog that fired anywhere on this device (P.err != 0): waiting workgroups give up at
+// once instead of each running into its own watchdog (a lost hand-off fails in seconds).
+__device__ __forceinline__ bool st_failed(const StParams &P)
+{
+    return __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
 // low word of a granule published for this sweep (bounded spin; error bit 4 on timeout)
 __device__ __forceinline__ uint32_t st_inbox_word(const StParams &P, const unsigned long long *p)
 {
     for (unsigned spins = 0;; ++spins) {
         const unsigned long long g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (st_granule_ready(g, P.epoch)) return (uint32_t)g;
-        if (spins > ST_WATCHDOG) {
+        if ((spins & 255u) == 255u && st_failed(P)) return 0xffffffffu;
+        if (spins > ST_WATCHDOG / 4) {
             atomicOr(P.err, 4);
             atomicMax(P.err + 1, P.sweep + 1);
             return 0xffffffffu;
@@ -216,7 +224,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         }
     }
     for (;;) {
-        if (tid == 0) s_task = atomicAdd(P.queue, 1);
+        if (tid == 0) s_task = st_failed(P) ? P.ntasks : atomicAdd(P.queue, 1);
         __syncthreads();
         const int task = s_task;
         if (task >= P.ntasks) break;
@@ -326,7 +334,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                     ++n_cpoll;
                     if (!__all(own_ok)) ++n_cpoll_own;
-                    if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
+                    if (++polls > ST_WATCHDOG || lds_ld(&s_abort) || ((polls & 1023u) == 0u && st_failed(P))) {
                         if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
                         h = nsteps;
                         break;
@@ -547,7 +555,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                              st_granule_ready(__hip_atomic_load(hsrc + hA, __ATOMIC_RELAXED, GSCOPE), P.epoch);
                     if (!__any(go)) {
                         ++n_hpoll;
-                        if (++idle > ST_WATCHDOG) {
+                        if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
                             if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
                             break;
                         }
@@ -652,7 +660,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     // back off (64..1024 cycles): hundreds of waiting tiles must not flood the
                     // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
                     ++n_hpoll;
-                    if (++idle > ST_WATCHDOG) {
+                    if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
                         if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
                         break;
                     }

@@ -37,7 +37,7 @@ def slab_range(nk: int, world: int, rank: int) -> tuple[int, int]:
 def _dist():
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized():
-        raise RuntimeError("sdfgen_amd.distributed needs an initialised torch.distributed process group")
+        raise RuntimeError("sdfgenfast_amd.distributed needs an initialised torch.distributed process group")
     return dist
 
 

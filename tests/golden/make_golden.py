@@ -10,7 +10,7 @@ Every expected output comes from ``sdfgen::cpu::make_level_set3(..., num_threads
 (/root/reference/cpu_lib/makelevelset3.cpp:192, compiled by oracle/Makefile into
 oracle/_ref/libsdfref.so).  Inputs are the reference's own test meshes
 (tests/resources, tests/test_correctness.cpp:30-62) plus deterministic synthetic
-meshes from sdfgen_amd/meshgen.py.  Only data (inputs + outputs) is stored.
+meshes from sdfgenfast_amd/meshgen.py.  Only data (inputs + outputs) is stored.
 """
 from __future__ import annotations
 
@@ -28,7 +28,7 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from oracle import oracle as O  # noqa: E402
-from sdfgen_amd import meshgen, meshio  # noqa: E402
+from sdfgenfast_amd import meshgen, meshio  # noqa: E402
 
 RES = "/root/reference/tests/resources"
 

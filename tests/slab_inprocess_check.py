@@ -14,7 +14,7 @@ import numpy as np  # noqa: E402
 
 from conftest import bits_equal, diff_report  # noqa: E402
 from oracle import oracle as O  # noqa: E402
-from sdfgen_amd import _hiprt, _lib, meshgen  # noqa: E402
+from sdfgenfast_amd import _hiprt, _lib, meshgen  # noqa: E402
 
 
 def main():

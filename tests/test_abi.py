@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import ROOT
-from sdfgen_amd import _lib
+from sdfgenfast_amd import _lib
 
 
 def declared_functions():

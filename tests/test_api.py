@@ -1,4 +1,4 @@
-"""The Python drop-in (sdfgen_amd, also importable as `sdfgen`) mirrors the
+"""The Python drop-in (sdfgenfast_amd, also importable as `sdfgen`) mirrors the
 reference's own Python tests (python/tests/test_sdfgen.py, 9 classes / 51 tests):
 same call shapes, defaults, dtype conversions and error contracts.  These run
 on CPU (backend "cpu", or "auto" on a GPU-less host); the GPU path is covered
@@ -9,8 +9,8 @@ import tempfile
 import numpy as np
 import pytest
 
-import sdfgen  # the drop-in package name (sdfgen/__init__.py re-exports sdfgen_amd)
-import sdfgen_amd
+import sdfgen  # the drop-in package name (sdfgen/__init__.py re-exports sdfgenfast_amd)
+import sdfgenfast_amd
 from conftest import bits_equal
 
 
@@ -47,7 +47,7 @@ def temp_sdf_file():
 
 
 def test_sdfgen_alias_is_the_same_package():
-    assert sdfgen.generate_sdf is sdfgen_amd.generate_sdf
+    assert sdfgen.generate_sdf is sdfgenfast_amd.generate_sdf
     for name in ("load_mesh", "generate_sdf", "save_sdf", "load_sdf", "is_gpu_available",
                  "generate_from_mesh", "generate_from_file"):
         assert hasattr(sdfgen, name)

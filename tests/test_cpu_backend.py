@@ -6,7 +6,7 @@ import pytest
 
 from conftest import bits_equal, diff_report
 from oracle import oracle as O
-from sdfgen_amd import _lib, meshgen
+from sdfgenfast_amd import _lib, meshgen
 
 
 @pytest.mark.parametrize("threads", [1, 2, 5, 8])

@@ -1,4 +1,4 @@
-"""Multi-process Z-slab path on CPU (gloo, world sizes 2 and 3): sdfgen_amd.distributed.
+"""Multi-process Z-slab path on CPU (gloo, world sizes 2 and 3): sdfgenfast_amd.distributed.
 
 The same slab split, plane hand-off order and gather as the GPU ranks use; the planes
 travel with send/recv over gloo.  Bit-exact against the oracle.
@@ -12,7 +12,7 @@ import torch.multiprocessing as tmp
 
 from conftest import bits_equal, diff_report
 from oracle import oracle as O
-from sdfgen_amd import meshgen
+from sdfgenfast_amd import meshgen
 
 
 def _free_port():
@@ -23,7 +23,7 @@ def _free_port():
 
 def _worker(rank, world, port, dims, result_path):
     import torch.distributed as dist
-    from sdfgen_amd import distributed as D
+    from sdfgenfast_amd import distributed as D
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         v, t = meshgen.bumpy_sphere(40, 17)
@@ -52,7 +52,7 @@ def test_cpu_slabs_over_gloo_match_oracle(tmp_path, world, dims):
 
 def test_cpu_slab_session_single_process_chain():
     """Drive all slabs of a grid from one process, handing the planes on by hand."""
-    from sdfgen_amd import _lib
+    from sdfgenfast_amd import _lib
     dims = (15, 13, 11)
     v, t = meshgen.bumpy_sphere(30, 13)
     o, dx = meshgen.grid_mode2b(v, *(max(d, 8) for d in dims), 2)
@@ -74,7 +74,7 @@ def test_cpu_slab_session_single_process_chain():
 
 
 def test_slab_range_partition():
-    from sdfgen_amd.distributed import slab_range
+    from sdfgenfast_amd.distributed import slab_range
     for nk, w in [(256, 8), (29, 3), (10, 4), (512, 7)]:
         rs = [slab_range(nk, w, r) for r in range(w)]
         assert rs[0][0] == 0 and rs[-1][1] == nk

@@ -1,4 +1,4 @@
-"""sdfgen_amd.distributed on the GPU: 2 ranks (torch.distributed, gloo control plane) on
+"""sdfgenfast_amd.distributed on the GPU: 2 ranks (torch.distributed, gloo control plane) on
 the box's one GPU, inboxes mapped over HIP IPC; and bench.py's multi-rank mode."""
 import os
 import socket
@@ -11,7 +11,7 @@ import torch.multiprocessing as tmp
 
 from conftest import bits_equal, diff_report
 from oracle import oracle as O
-from sdfgen_amd import meshgen
+from sdfgenfast_amd import meshgen
 
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -27,7 +27,7 @@ def _worker(rank, world, port, dims, result_path):
     os.environ["SDFGEN_TILE_GRID"] = "64"   # both ranks share one GPU here: keep both resident
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    from sdfgen_amd import distributed as D
+    from sdfgenfast_amd import distributed as D
     try:
         v, t = meshgen.bumpy_sphere(90, 31)
         o, dx = meshgen.grid_mode2b(v, *dims, 2)

@@ -15,7 +15,7 @@ import pytest
 
 from conftest import GOLDEN, bits_equal, diff_report
 from oracle import oracle as O
-from sdfgen_amd import _lib, meshgen
+from sdfgenfast_amd import _lib, meshgen
 
 pytestmark = pytest.mark.gpu
 
@@ -74,7 +74,7 @@ def test_gpu_matches_reference_fixture(golden_case, layout):
 
 
 def test_gpu_generate_sdf_api(golden_case):
-    import sdfgen_amd as S
+    import sdfgenfast_amd as S
     c = golden_case
     got = S.generate_sdf(c.vertices, c.triangles, tuple(c.origin), c.dx, *c.dims, exact_band=c.exact_band,
                          backend="gpu")

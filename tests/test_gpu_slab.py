@@ -16,7 +16,7 @@ import pytest
 
 from conftest import bits_equal, diff_report
 from oracle import oracle as O
-from sdfgen_amd import meshgen
+from sdfgenfast_amd import meshgen
 
 pytestmark = pytest.mark.gpu
 
@@ -37,7 +37,7 @@ def _cap_grid(monkeypatch):
 # so in-process tests use 2 slabs and the 3-4 slab layouts run one process per slab.
 @pytest.mark.parametrize("nslabs,dims", [(2, (40, 36, 44)), (2, (33, 41, 29)), (2, (9, 9, 4)), (2, (17, 5, 60))])
 def test_slabs_one_process_match_oracle(nslabs, dims):
-    from sdfgen_amd import _hiprt, _lib
+    from sdfgenfast_amd import _hiprt, _lib
     v, t, o, dx, dims = _mesh(dims=dims)
     ni, nj, nk = dims
     want = np.asfortranarray(O.make_level_set3(v, t, o, dx, ni, nj, nk, 1))
@@ -57,7 +57,7 @@ def test_slabs_one_process_match_oracle(nslabs, dims):
 
 
 def test_slab_kfast_layout_and_host_run():
-    from sdfgen_amd import _lib
+    from sdfgenfast_amd import _lib
     v, t, o, dx, dims = _mesh()
     ni, nj, nk = dims
     want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, ni, nj, nk, 1))
@@ -66,7 +66,7 @@ def test_slab_kfast_layout_and_host_run():
     slabs[1].connect_local(slabs[0], None)
     # host-array entry runs one slab at a time: run slab 0's producer side by enqueueing
     # the device path for slab 1 first is not possible with run(); use enqueue for both
-    from sdfgen_amd import _hiprt
+    from sdfgenfast_amd import _hiprt
     dv, dt = _hiprt.DeviceBuffer.from_array(v), _hiprt.DeviceBuffer.from_array(t)
     outs = [_hiprt.DeviceBuffer(ni * nj * (sl.k_end - sl.k_begin) * 4) for sl in slabs]
     for sl, d in zip(slabs, outs):
@@ -80,7 +80,7 @@ def test_slab_kfast_layout_and_host_run():
 
 
 def test_slab_validation():
-    from sdfgen_amd import _lib
+    from sdfgenfast_amd import _lib
     with pytest.raises(ValueError):
         _lib.Slab(0, 3, 0, 10, 10, 5)      # fewer than 2 planes per slab
     with pytest.raises(ValueError):
@@ -92,7 +92,7 @@ def test_slab_validation():
 
 def _ipc_worker(nslabs, slab, dims, q_out, q_in, barrier, res):
     os.environ["SDFGEN_TILE_GRID"] = "64"
-    from sdfgen_amd import _lib
+    from sdfgenfast_amd import _lib
     v, t, o, dx, dims = _mesh(dims=dims)
     sl = _lib.Slab(0, nslabs, slab, *dims)
     q_out.put((slab, sl.export()))

@@ -14,7 +14,7 @@ import pytest
 
 from conftest import bits_equal, diff_report
 from oracle import oracle as O
-from sdfgen_amd import meshgen
+from sdfgenfast_amd import meshgen
 
 
 def test_oracle_matches_reference_fixtures(golden_case):

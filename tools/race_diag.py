@@ -6,7 +6,7 @@ import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 from oracle import oracle as O
-from sdfgen_amd import _lib, meshgen
+from sdfgenfast_amd import _lib, meshgen
 
 v, t = meshgen.bumpy_sphere(120, 41)
 dims = (48, 40, 56)

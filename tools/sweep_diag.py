@@ -7,7 +7,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
-from sdfgen_amd import _lib, meshgen  # noqa: E402
+from sdfgenfast_amd import _lib, meshgen  # noqa: E402
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c3_sphere1m_256"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 2

@@ -1,7 +1,7 @@
 """Per-sweep device times and sparse-repair statistics for one workload (diagnostics)."""
 import os, sys, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from sdfgen_amd import _lib, meshgen
+from sdfgenfast_amd import _lib, meshgen
 
 name = sys.argv[1] if len(sys.argv) > 1 else "c3_sphere1m_256"
 v, t, o, dx, dims = meshgen.workload(name)

@@ -2,7 +2,7 @@
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
-from sdfgen_amd import _lib, meshgen
+from sdfgenfast_amd import _lib, meshgen
 name = sys.argv[1] if len(sys.argv) > 1 else "c3_sphere1m_256"
 sw = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 v, t, o, dx, dims = meshgen.workload(name)
