@@ -52,16 +52,32 @@ def test_distributed_gpu_two_ranks_match_oracle(tmp_path, dims):
     assert bits_equal(got, want), diff_report(got, want, dx)
 
 
-def test_bench_two_ranks_zslab_parity():
-    """bench.py under torch.distributed.run with 2 ranks on one GPU: slab mode, bit-exact."""
+def _bench_two_ranks(*extra):
     env = dict(os.environ, SDFGEN_TILE_GRID="64", HSA_ENABLE_IPC_MODE_LEGACY="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "1", "--warmup", "0", "--workload", "c2_sphere70k_128"]
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--workload", "c2_sphere70k_128", *extra]
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     line = [x for x in r.stdout.splitlines() if x.startswith("{")][-1]
     import json
-    res = json.loads(line)
+    return json.loads(line)
+
+
+def test_bench_two_ranks_zslab_parity():
+    """bench.py --mode zslab under torch.distributed.run, 2 ranks on one GPU: bit-exact."""
+    res = _bench_two_ranks("--mode", "zslab", "--no-zslab")
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "zslab2" and res["scaling"] == "strong"
     assert res["parity"] == "bit-exact vs reference (sha256 of phi)", res
+    assert "zslab" not in res
+
+
+def test_bench_two_ranks_replicas_with_zslab_child():
+    """Default multi-rank mode: replicas (weak scaling) plus the Z-slab side measurement
+    run as a child torch.distributed job; both bit-exact."""
+    res = _bench_two_ranks("--zslab-workload", "c2_sphere70k_128")
+    assert res["config"]["parallelism"] == "replicas2" and res["scaling"] == "weak", res
+    assert res["parity"] == "bit-exact vs reference (sha256 of phi)", res
+    zs = res["zslab"]
+    assert "error" not in zs, zs
+    assert zs["parallelism"] == "zslab2" and zs["parity"] == "bit-exact vs reference (sha256 of phi)", zs
