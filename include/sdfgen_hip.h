@@ -64,7 +64,12 @@ int sdfgen_hip_device_count(void);
  *   xyz      : nvert x 3 float32 positions   (std::vector<Vec3f>::data())
  *   origin   : grid origin (3 floats); dx: cell size; ni,nj,nk: grid dims (> 0)
  *   exact_band: band half-width in cells (cpu_lib/makelevelset3.cpp:210-212)
- *   ngpu     : devices to use (0 = all visible; the grid is split into Z-slabs)
+ *   ngpu     : devices to use.  0 or 1 = the current device.  n > 1 = devices 0..n-1, the
+ *              grid split into n Z-slabs driven from this thread (sdfgen_hip_slab_*
+ *              sessions connected in-process over peer memory); at most
+ *              nk/2 slabs, ENODEV if fewer than n devices are visible.  0 does not mean
+ *              "all devices": one grid is bound by the sweeps' dependency chain, so
+ *              more GPUs pay off only for large grids.
  *   out_layout: SDFGEN_LAYOUT_*
  *   phi_out  : caller-allocated ni*nj*nk floats
  */

@@ -13,6 +13,7 @@ mode 2a :109-131; mode 2b :150-176, dx = max over axes), the same output names
 
 Additions for this backend (options go before the positional arguments):
   --backend {auto,gpu,cpu}   hardware selection (reference: always Auto, :255)
+  --gpus N                   split the grid into N Z-slabs over GPUs 0..N-1 (GPU backend)
   -o/--output PATH           output file instead of the derived name
   -q/--quiet                 summary line only
 The VTK writer of the reference (HAVE_VTK builds) is out of scope.
@@ -139,6 +140,7 @@ def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(prog="python -m sdfgenfast_amd", add_help=True,
                                  description="SDFGen on MI355X (see module docstring for the modes)")
     ap.add_argument("--backend", choices=["auto", "gpu", "cpu"], default="auto")
+    ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("-o", "--output", default=None)
     ap.add_argument("-q", "--quiet", action="store_true")
     ap.add_argument("args", nargs=argparse.REMAINDER)
@@ -158,7 +160,12 @@ def main(argv: list[str] | None = None) -> int:
     say(f"  Padded bounds: ({origin[0]:.6g}, {origin[1]:.6g}, {origin[2]:.6g})")
     say(f"  Implementation: {impl}")
     t0 = time.perf_counter()
-    sdf = generate_sdf(v, t, origin, float(dx), *dims, exact_band=1, backend=ns.backend, num_threads=p["threads"])
+    if ns.gpus > 1 and ns.backend != "cpu":
+        impl = f"GPU (HIP, MI355X) x{ns.gpus} Z-slabs"
+        sdf = _lib.make_level_set3(v, t, origin, float(dx), *dims, 1, _lib.LAYOUT_KFAST, ngpu=ns.gpus)
+    else:
+        sdf = generate_sdf(v, t, origin, float(dx), *dims, exact_band=1, backend=ns.backend,
+                           num_threads=p["threads"])
     el = time.perf_counter() - t0
     out = ns.output or output_name(p, dims)
     inside = meshio.write_sdf(out, sdf, origin, float(dx))

@@ -832,6 +832,80 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
     return 0;
 }
 
+// ngpu > 1 in sdfgen_hip_make_level_set3: one Z-slab session per device (0..n-1), connected
+// in-process, driven from this thread.  Every slab's kernels are enqueued before any result is
+// copied back: a slab's sweeps wait on its neighbours' planes, and a D2H copy into pageable
+// memory blocks the host until its slab has finished.
+// SDFGEN_DEBUG_SLABS_ONE_DEVICE (diagnostics/tests on a one-GPU box): every slab on device 0;
+// then SDFGEN_TILE_GRID must cap the persistent grids so all slabs stay co-resident.
+}  // namespace
+
+struct sdfgen_hip_slab {
+    SlabSession s;
+};
+
+namespace {
+
+struct SlabRef {
+    sdfgen_hip_slab *h = nullptr;
+};
+SlabSession *slab_of(sdfgen_hip_slab *h) { return &h->s; }
+
+int run_zslab_local(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert, const float origin[3],
+                    float dx, int ni, int nj, int nk, int band, int n, int layout, float *phi_out, Err &err)
+{
+    const bool one_dev = getenv("SDFGEN_DEBUG_SLABS_ONE_DEVICE") != nullptr;
+    std::vector<SlabRef> S(n);
+    struct Cleanup {
+        std::vector<SlabRef> &s;
+        ~Cleanup()
+        {
+            for (auto &r : s) sdfgen_hip_slab_destroy(r.h);
+        }
+    } cleanup{S};
+    int rc;
+    for (int g = 0; g < n; ++g)
+        if ((rc = sdfgen_hip_slab_create(one_dev ? 0 : g, n, g, ni, nj, nk, &S[g].h, err.buf, err.len))) return rc;
+    for (int g = 0; g < n; ++g)
+        if ((rc = sdfgen_hip_slab_connect_local(S[g].h, g > 0 ? S[g - 1].h : nullptr,
+                                                g < n - 1 ? S[g + 1].h : nullptr, err.buf, err.len)))
+            return rc;
+    for (int g = 0; g < n; ++g) {
+        SlabSession *T = slab_of(S[g].h);
+        HIPCHK(hipSetDevice(T->device));
+        const uint64_t nout = (uint64_t)ni * nj * (T->k_end - T->k_begin);
+        HIPCHK(hipMalloc((void **)&T->tri, std::max<size_t>(12 * ntri, 16)));
+        T->cap_tri = 12 * ntri;
+        HIPCHK(hipMalloc((void **)&T->xyz, std::max<size_t>(12 * nvert, 16)));
+        T->cap_xyz = 12 * nvert;
+        HIPCHK(hipMalloc((void **)&T->out, std::max<size_t>(4 * nout, 16)));
+        T->cap_out = 4 * nout;
+        if (ntri) HIPCHK(hipMemcpyAsync(T->tri, tri, 12 * ntri, hipMemcpyHostToDevice, T->stream));
+        if (nvert) HIPCHK(hipMemcpyAsync(T->xyz, xyz, 12 * nvert, hipMemcpyHostToDevice, T->stream));
+        if ((rc = slab_enqueue(T, T->tri, ntri, T->xyz, nvert, origin, dx, band, layout, T->out, err))) return rc;
+    }
+    for (int g = 0; g < n; ++g) {   // slab results into the caller's grid
+        SlabSession *T = slab_of(S[g].h);
+        HIPCHK(hipSetDevice(T->device));
+        const size_t nks = (size_t)(T->k_end - T->k_begin);
+        if (layout == SDFGEN_LAYOUT_ARRAY3)   // i-fastest: the slab's planes are one contiguous range
+            HIPCHK(hipMemcpyAsync(phi_out + (size_t)T->k_begin * ni * nj, T->out, 4 * nks * ni * nj,
+                                  hipMemcpyDeviceToHost, T->stream));
+        else   // k-fastest: rows of nks values land at stride nk
+            HIPCHK(hipMemcpy2DAsync(phi_out + T->k_begin, 4 * (size_t)nk, T->out, 4 * nks, 4 * nks,
+                                    (size_t)ni * nj, hipMemcpyDeviceToHost, T->stream));
+    }
+    int first = 0;
+    for (int g = 0; g < n; ++g) {   // collect every slab's status, report the first failure
+        Err e2{nullptr, 0};
+        SlabSession *T = slab_of(S[g].h);
+        HIPCHK(hipSetDevice(T->device));
+        rc = slab_finish(T, nvert, nullptr, first ? e2 : err);
+        if (rc && !first) first = rc;
+    }
+    return first;
+}
+
 }  // namespace
 
 extern "C" {
@@ -852,7 +926,13 @@ int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
         return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
     const int ndev = device_count_impl();
     if (ndev <= 0) return err.set(SDFGEN_HIP_ENODEV, "GPU backend requested but no HIP GPU device is available");
-    (void)ngpu;  // multi-device Z-slab path: see DESIGN.md (single device in this build)
+    if (ngpu > 1 && nk >= 4) {
+        const int n = std::min(ngpu, nk / 2);
+        if (ngpu > ndev && !getenv("SDFGEN_DEBUG_SLABS_ONE_DEVICE"))
+            return err.set(SDFGEN_HIP_ENODEV, "ngpu = %d but only %d HIP device(s) visible", ngpu, ndev);
+        return run_zslab_local(tri, ntri, xyz, nvert, origin, dx, ni, nj, nk, exact_band, n, out_layout, phi_out,
+                               err);
+    }
     int dev = 0;
     HIPCHK(hipGetDevice(&dev));
     Workspace *ws = nullptr;
@@ -989,9 +1069,6 @@ int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *ou
 
 
 // ---------------------------------------------------------------- Z-slab sessions
-struct sdfgen_hip_slab {
-    SlabSession s;
-};
 
 int sdfgen_hip_slab_create(int device, int nslabs, int slab, int ni, int nj, int nk, sdfgen_hip_slab **out,
                            char *errbuf, size_t errlen)

@@ -141,3 +141,25 @@ def test_slabs_ipc_one_process_per_slab_match_oracle(nslabs, dims):
     got = np.concatenate([np.frombuffer(b, np.float32) for _, _, _, b, _ in parts]).reshape((ni, nj, nk), order="F")
     assert [p[4] for p in parts] == [3] * nslabs
     assert bits_equal(got, want), diff_report(got, want, dx)
+
+
+@pytest.mark.parametrize("layout", ["array3", "kfast"])
+def test_c_abi_ngpu_zslab_path_matches_oracle(monkeypatch, layout):
+    """sdfgen_hip_make_level_set3(ngpu=2): the in-process multi-device Z-slab path, with
+    both slabs placed on this box's one GPU (SDFGEN_DEBUG_SLABS_ONE_DEVICE) -- host
+    upload, enqueue-all-then-copy ordering and the strided k-fastest assembly."""
+    from sdfgenfast_amd import _lib
+    monkeypatch.setenv("SDFGEN_DEBUG_SLABS_ONE_DEVICE", "1")
+    v, t, o, dx, dims = _mesh(dims=(33, 41, 29))
+    want = O.make_level_set3(v, t, o, dx, *dims, 1)
+    lay = _lib.LAYOUT_ARRAY3 if layout == "array3" else _lib.LAYOUT_KFAST
+    got = _lib.make_level_set3(v, t, o, dx, *dims, 1, lay, ngpu=2)
+    assert bits_equal(got, want), diff_report(got, want, dx)
+
+
+def test_c_abi_ngpu_more_than_visible_is_enodev():
+    from sdfgenfast_amd import _lib
+    n = _lib.device_count()
+    v, t, o, dx, dims = _mesh(dims=(20, 20, 20))
+    with pytest.raises(RuntimeError, match="visible"):
+        _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_KFAST, ngpu=n + 1)
