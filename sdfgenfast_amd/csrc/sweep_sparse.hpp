@@ -28,7 +28,8 @@
 //     a runner reads labels only after the request it retires was observed: the first
 //     evaluation retires just the request that handed it the cell (written after the
 //     label that caused it), and every further round retires what its atomicSub saw.
-//   * ctl[PENDING] counts queued or running work items; workers leave when it is 0.
+//   * the high half of ctl[SP_QUEUE] counts queued or running work items (it grows in
+//     the same atomic as the ring tail); workers leave when it is 0.
 // Every spin is bounded (watchdog -> error bit, reported by the host).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -38,7 +39,11 @@
 
 namespace sdfhip {
 
-enum { SP_TAIL = 0, SP_HEAD = 1, SP_PENDING = 2, SP_ERR = 3, SP_ENQ = 4, SP_RUNS = 5, SP_NCTL = 8 };
+// ctl[SP_QUEUE]: work items appended to the ring (low 32 bits) and work items queued or
+// running (high 32 bits) in ONE word, so an append is one atomic round trip.
+enum { SP_QUEUE = 0, SP_HEAD = 1, SP_ERR = 3, SP_ENQ = 4, SP_RUNS = 5, SP_NCTL = 8 };
+constexpr unsigned long long SP_PENDING_ONE = 1ull << 32;
+constexpr unsigned long long SP_TAIL_LIMIT = 0xF0000000ull;   // appends per sweep (error beyond)
 constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
 constexpr int SP_WORKERS = 512;              // max one-wave workgroups of the repair kernel
 constexpr int SP_WORKERS_DEFAULT = 128;
@@ -123,6 +128,7 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
     bool changed = false;
     const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
     const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
+    bool ev[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
         const int t = lab[q];
@@ -130,13 +136,44 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
 #pragma unroll
         for (int r = 0; r < q; ++r) skip = skip || (lab[r] == t);
         skip = skip || (interior && lcq[q] <= P.seen[q]);   // seen[q] = -1: never
-        if (!skip) {
-            const float4 v0 = P.soup[3 * (size_t)t], v1 = P.soup[3 * (size_t)t + 1], v2 = P.soup[3 * (size_t)t + 2];
-            const float d = ptd(gx, mk3(v0.x, v0.y, v0.z), mk3(v1.x, v1.y, v1.z), mk3(v2.x, v2.y, v2.z));
-            if (d < phi) {
-                phi = d;
-                ct = t;
-                changed = true;
+        ev[q] = !skip;
+    }
+    if (LIVE) {
+        // The repair walks dependency chains one cell after another: issue every candidate's
+        // vertex gather at once (one memory round trip per cell, not one per candidate).
+        float4 v[7][3];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            const size_t b = 3 * (size_t)(ev[q] ? lab[q] : 0);
+            v[q][0] = P.soup[b];
+            v[q][1] = P.soup[b + 1];
+            v[q][2] = P.soup[b + 2];
+        }
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            if (ev[q]) {
+                const float d = ptd(gx, mk3(v[q][0].x, v[q][0].y, v[q][0].z), mk3(v[q][1].x, v[q][1].y, v[q][1].z),
+                                    mk3(v[q][2].x, v[q][2].y, v[q][2].z));
+                if (d < phi) {
+                    phi = d;
+                    ct = lab[q];
+                    changed = true;
+                }
+            }
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 7; ++q) {
+            if (ev[q]) {
+                const int t = lab[q];
+                const float4 v0 = P.soup[3 * (size_t)t], v1 = P.soup[3 * (size_t)t + 1],
+                             v2 = P.soup[3 * (size_t)t + 2];
+                const float d = ptd(gx, mk3(v0.x, v0.y, v0.z), mk3(v1.x, v1.y, v1.z), mk3(v2.x, v2.y, v2.z));
+                if (d < phi) {
+                    phi = d;
+                    ct = t;
+                    changed = true;
+                }
             }
         }
     }
@@ -144,12 +181,6 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
     return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
 }
 
-__device__ __forceinline__ void sp_enqueue(const SpParams &P, size_t e)
-{
-    atomicAdd(&P.ctl[SP_PENDING], 1ull);
-    const unsigned long long t = atomicAdd(&P.ctl[SP_TAIL], 1ull);
-    sp_st32(P.queue + t % P.cap, (unsigned)(e + 1));
-}
 
 // Request rechecks of the downstream neighbours of (i,j,k) (the cells whose upwind set
 // contains it).  Returns the first cell this call took ownership of when `claim`, so
@@ -182,8 +213,10 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
         else ++nq;
     }
     if (nq) {
-        atomicAdd(&P.ctl[SP_PENDING], (unsigned long long)nq);
-        unsigned long long t = atomicAdd(&P.ctl[SP_TAIL], (unsigned long long)nq);
+        // pending and tail grow together, so no item is visible to a worker before it counts
+        const unsigned long long old_q = atomicAdd(&P.ctl[SP_QUEUE], nq * SP_PENDING_ONE + nq);
+        unsigned long long t = old_q & 0xffffffffull;
+        if (t + nq > SP_TAIL_LIMIT) atomicOr(&P.ctl[SP_ERR], 2ull);
 #pragma unroll
         for (int q = 0; q < 7; ++q)
             if (old[q] == 0u && tgt[q] != mine) sp_st32(P.queue + (t++) % P.cap, (unsigned)(tgt[q] + 1));
@@ -247,7 +280,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 rq = 1;
                 waiting = false;
                 spins = 0;
-            } else if (sp_ld64(&P.ctl[SP_PENDING]) == 0ull) {
+            } else if ((sp_ld64(&P.ctl[SP_QUEUE]) >> 32) == 0ull) {
                 done = true;   // nothing queued or running anywhere: no slot can fill any more
             } else if (++spins > SP_WATCHDOG) {
                 atomicOr(&P.ctl[SP_ERR], 1ull);
@@ -282,7 +315,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 } else {
                     e = NONE;
                     sp_order();
-                    atomicSub(&P.ctl[SP_PENDING], 1ull);
+                    atomicSub(&P.ctl[SP_QUEUE], SP_PENDING_ONE);
                 }
             } else {
                 rq = old - rq;   // evaluate again for the requests that arrived meanwhile

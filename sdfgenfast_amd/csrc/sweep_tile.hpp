@@ -135,9 +135,20 @@ __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
 
 // A watchdog that fired anywhere on this device (P.err != 0): waiting workgroups give up at
 // once instead of each running into its own watchdog (a lost hand-off fails in seconds).
+#ifndef ST_FASTFAIL
+#define ST_FASTFAIL 1
+#endif
 __device__ __forceinline__ bool st_failed(const StParams &P)
 {
-    return __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    return ST_FASTFAIL && __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+// Record a fired watchdog and close the task queue: later claims all fall past the end.
+__device__ __forceinline__ void st_fail(const StParams &P, int bit)
+{
+    atomicOr(P.err, bit);
+    atomicMax(P.err + 1, P.sweep + 1);
+    atomicMax(P.queue, P.ntasks);
 }
 
 // low word of a granule published for this sweep (bounded spin; error bit 4 on timeout)
@@ -148,8 +159,7 @@ __device__ __forceinline__ uint32_t st_inbox_word(const StParams &P, const unsig
         if (st_granule_ready(g, P.epoch)) return (uint32_t)g;
         if ((spins & 255u) == 255u && st_failed(P)) return 0xffffffffu;
         if (spins > ST_WATCHDOG / 4) {
-            atomicOr(P.err, 4);
-            atomicMax(P.err + 1, P.sweep + 1);
+            st_fail(P, 4);
             return 0xffffffffu;
         }
         __builtin_amdgcn_s_sleep(4);
@@ -224,7 +234,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         }
     }
     for (;;) {
-        if (tid == 0) s_task = st_failed(P) ? P.ntasks : atomicAdd(P.queue, 1);
+        if (tid == 0) s_task = atomicAdd(P.queue, 1);   // a fired watchdog pushes the counter past the end
         __syncthreads();
         const int task = s_task;
         if (task >= P.ntasks) break;
@@ -334,8 +344,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                     ++n_cpoll;
                     if (!__all(own_ok)) ++n_cpoll_own;
-                    if (++polls > ST_WATCHDOG || lds_ld(&s_abort) || ((polls & 1023u) == 0u && st_failed(P))) {
-                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
+                    if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
+                        if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
                         h = nsteps;
                         break;
                     }
@@ -556,7 +566,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     if (!__any(go)) {
                         ++n_hpoll;
                         if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
-                            if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
+                            if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
                             break;
                         }
                         if (idle < 4) __builtin_amdgcn_s_sleep(1);
@@ -661,7 +671,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
                     ++n_hpoll;
                     if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
-                        if (L == 0) { lds_st(&s_abort, 1); atomicOr(P.err, 2); atomicMax(P.err + 1, P.sweep + 1); }
+                        if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
                         break;
                     }
                     if (idle < 4) __builtin_amdgcn_s_sleep(1);
