@@ -136,6 +136,38 @@ SDF_HD float ptd_nb(f3 x0, f3 x1, f3 x2, f3 x3)
     return inside ? d_in : d_edge;
 }
 
+// ptd_nb for a wave evaluating many (point, triangle) pairs at once: the inside-projection
+// block and the two-segment block each run only if some active lane needs it (wave-uniform
+// branches).  Every lane still performs exactly ptd_nb's operations for the case it takes,
+// so the result is bit-identical; away from the surface (points project outside the tiny
+// triangles) whole waves skip the inside block.
+__device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3)
+{
+    f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3), x03 = sub3(x0, x3);
+    float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
+    float invdet = div_rn(1.0f, fmax_std(m13 * m23 - d * d, 1e-30f));
+    float a = dot3(x13, x03), b = dot3(x23, x03);
+    float w23 = invdet * (m23 * a - d * b);
+    float w31 = invdet * (m13 * b - d * a);
+    float w12 = (1.0f - w23) - w31;
+    const bool inside = (w23 >= 0.0f) & (w31 >= 0.0f) & (w12 >= 0.0f);
+    float r = 0.0f;
+    if (__any(inside)) {
+        f3 p = mk3((x1.x * w23 + x2.x * w31) + x3.x * w12,
+                   (x1.y * w23 + x2.y * w31) + x3.y * w12,
+                   (x1.z * w23 + x2.z * w31) + x3.z * w12);
+        r = dist3(x0, p);
+    }
+    if (__any(!inside)) {
+        const bool c23 = w23 > 0.0f, c31 = !c23 & (w31 > 0.0f);
+        const f3 fb = (c23 | c31) ? x2 : x3;
+        const f3 sa = c23 ? x1 : x2;
+        const float d_edge = fmin_std(psd(x0, x1, fb), psd(x0, sa, x3));
+        r = inside ? r : d_edge;
+    }
+    return r;
+}
+
 // orientation (SOS-robust 2D), FP64.
 SDF_HD int orientation(double x1, double y1, double x2, double y2, double &area)
 {

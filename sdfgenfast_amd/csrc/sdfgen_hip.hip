@@ -350,7 +350,7 @@ __global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__
     const float *p = pts + 12 * q;
     const f3 x0 = mk3(p[0], p[1], p[2]), x1 = mk3(p[3], p[4], p[5]), x2 = mk3(p[6], p[7], p[8]),
              x3 = mk3(p[9], p[10], p[11]);
-    out[q] = variant == 0 ? ptd(x0, x1, x2, x3) : ptd_nb(x0, x1, x2, x3);
+    out[q] = variant == 0 ? ptd(x0, x1, x2, x3) : (variant == 1 ? ptd_nb(x0, x1, x2, x3) : ptd_wave(x0, x1, x2, x3));
 }
 
 __global__ void k_debug_pit2d(uint64_t n, const double *__restrict__ in, double *__restrict__ out)

@@ -78,7 +78,8 @@ constexpr int ST_RR = ST_RR_DEF;
 constexpr int ST_RO = ST_RO_DEF;
 constexpr int ST_RH = ST_RH_DEF;
 constexpr int ST_G = ST_G_DEF;
-static_assert(ST_NCW >= 1 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
+static_assert(ST_NCW >= 1 && ST_NCW <= 3 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
+typedef int i4v __attribute__((ext_vector_type(4)));
 static_assert((ST_RR & (ST_RR - 1)) == 0 && ST_RR >= 4, "ring slots: power of two >= 4");
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
@@ -211,9 +212,12 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
     __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
     __shared__ float s_d[ST_NCW][7 * ST_CPW];      // per compute wave: distance of candidate q for lane
-    __shared__ int s_own_fill;              // own entries ready for steps < s_own_fill
-    __shared__ int s_halo_ready[ST_NSTREAM];  // halo entries < s_halo_ready[s] in LDS
-    __shared__ int s_prog[ST_NCW];          // steps completed by each compute wave
+    // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
+    // compute wave w -- one 16-byte word, so a readiness poll is one ds_read_b128.
+    __shared__ __attribute__((aligned(16))) int s_hdr[4];
+    // halo entries < s_halo_ready[s] are in LDS; the extra last word is never "not ready"
+    // (the stream index of lanes that read no halo stream)
+    __shared__ int s_halo_ready[ST_NSTREAM + 1];
     __shared__ int s_abort;
     __shared__ int s_task;
 
@@ -259,10 +263,11 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 s_ent[3 * e + 1] = v1;
                 s_ent[3 * e + 2] = v2;
             }
-            if (L == 0) s_prog[wave] = 0;
+            if (L == 0) s_hdr[1 + wave] = 0;
             if (wave == 0 && L == 0) {
-                s_own_fill = 0;
+                s_hdr[0] = 0;
                 s_abort = 0;
+                s_halo_ready[ST_NSTREAM] = 0x3fffffff;
             }
         } else if (L < ST_NSTREAM) {
             int hb_ = 0, hc_ = 0;
@@ -320,6 +325,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 else if (bl == 0) { halo(5, cl - 1); halo(6, cl - 1); }
                 else { halo(5, ST_T + bl - 1); halo(6, ST_T + bl - 1); }
             }
+            const int hsA = (bl == 0) ? cl : ST_NSTREAM, hsB = (cl == 0) ? ST_T + bl : ST_NSTREAM,
+                      hsC = (bl == 0 && cl == 0) ? 2 * ST_T : ST_NSTREAM;
             unsigned polls = 0;
             unsigned long long t_wait = 0, w_own = 0, w_halo = 0, t_comp = 0, c_comp = 0;   // trace-only
             for (int h = 0; h < nsteps; ++h) {
@@ -328,15 +335,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
                 unsigned long long tw0 = 0;
                 for (;;) {
-                    const bool own_ok = lds_ld(&s_own_fill) > h;
-                    bool ok = own_ok;
-                    if (w > 0 && lds_ld(&s_prog[w - 1]) < h) ok = false;
-                    if (w < ST_NCW - 1 && lds_ld(&s_prog[w + 1]) < h - P.lead) ok = false;
-                    if (act) {
-                        if (bl == 0 && lds_ld(&s_halo_ready[cl]) <= a) ok = false;
-                        if (cl == 0 && lds_ld(&s_halo_ready[ST_T + bl]) <= a) ok = false;
-                        if (bl == 0 && cl == 0 && lds_ld(&s_halo_ready[2 * ST_T]) <= a) ok = false;
-                    }
+                    // branch-free: one 16-byte header read + the (up to 3) halo streams this
+                    // lane reads at this step (the dummy word for lanes off the tile edge)
+                    const i4v H = *reinterpret_cast<volatile i4v *>(s_hdr);
+                    const int rA = lds_ld(&s_halo_ready[hsA]), rB = lds_ld(&s_halo_ready[hsB]),
+                              rC = lds_ld(&s_halo_ready[hsC]);
+                    const bool own_ok = H.x > h;
+                    const int pm = (w == 1) ? H.y : ((w == 2) ? H.z : H.w);   // prog[w-1] (w > 0)
+                    const int pp = (w == 0) ? H.y : ((w == 1) ? H.z : H.w);   // prog[w+1]
+                    const bool ok = own_ok & ((w == 0) | (pm >= h)) & ((w == ST_NCW - 1) | (pp >= h - P.lead)) &
+                                    (!act | (min(rA, min(rB, rC)) > a));
                     if (__all(ok)) break;
                     if (TRACE && P.trace && tw0 == 0) {
                         tw0 = wall_clock64();
@@ -385,12 +393,12 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     // interior cells took part in every earlier sweep (sweep_sparse.hpp: exact skip)
                     const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
 #pragma unroll
-                    for (int q = 0; q < 7; ++q) {
-                        bool skip = (lab[q] < 0) || (lab[q] == ct_orig);
+                    for (int q = 0; q < 7; ++q) {   // bitwise, no short-circuit branches
+                        bool skip = (lab[q] < 0) | (lab[q] == ct_orig);
 #pragma unroll
-                        for (int r = 0; r < q; ++r) skip = skip || (lab[r] == lab[q]);
-                        skip = skip || (interior && lcq[q] <= P.seen[q]);   // seen[q] = -1: never
-                        if (!skip) fmask |= 1u << q;
+                        for (int r = 0; r < q; ++r) skip = skip | (lab[r] == lab[q]);
+                        skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
+                        fmask |= (skip ? 0u : 1u) << q;
                     }
                 }
                 // ---- at most one candidate per cell (the common case away from the surface):
@@ -405,7 +413,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                                 e1 = ent[q];
                                 t1 = lab[q];
                             }
-                        const float d = ptd_nb(st_gx(P, a, b, c), st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]),
+                        const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]),
                                                st_xyz(s_ent[3 * e1 + 2]));
                         if (d < phi) {
                             phi = d;
@@ -440,13 +448,13 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         const int l2 = p2 & 63, e2 = p2 >> 9;
                         const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
                                             c0 + ST_CLW * w + (l2 >> 3));
-                        const float d1 = ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
-                        const float d2 = ptd_nb(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
+                        const float d1 = ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
+                        const float d2 = ptd_wave(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
                         if (has2) s_d[w][((p2 >> 6) & 7) * ST_CPW + l2] = d2;
                     } else {
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] =
-                            ptd_nb(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
+                            ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
@@ -490,7 +498,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     c_comp += clock64() - cc0;
                 }
                 lds_drain();
-                if (L == 0) lds_st(&s_prog[w], h + 1);
+                if (L == 0) lds_st(&s_hdr[1 + w], h + 1);
                 if (TRACE && P.trace && w == 0 && L == 0 && (h == 0 || h == nsteps / 2))
                     P.trace[8 * task + (h == 0 ? 1 : 2)] = wall_clock64();
             }
@@ -547,9 +555,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             for (;;) {
                 // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
                 // may finish step h while wave w-1 is still on step h (it needs only h-1 of it).
-                int prog = lds_ld(&s_prog[0]);
+                int prog = lds_ld(&s_hdr[1]);
 #pragma unroll
-                for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_prog[w]));
+                for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_hdr[1 + w]));
                 if (lds_ld(&s_abort)) break;
                 if (idle && gA == 0 && hcA == 0) {
                     // Nothing in flight and the last round found nothing to do: wait cheaply (LDS
@@ -657,7 +665,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
 #undef ST_ISSUE
 #undef ST_LAND
                 lds_drain();
-                if (L == 0 && gA) lds_st(&s_own_fill, fB);
+                if (L == 0 && gA) lds_st(&s_hdr[0], fB);
                 if (hvalid && hp) lds_st(&s_halo_ready[L], hB);
                 const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
                 fA = fB; gA = gB; hA = hB; hcA = hcB;
