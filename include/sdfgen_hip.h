@@ -164,8 +164,9 @@ int sdfgen_hip_slab_destroy(sdfgen_hip_slab *s);
 /* Diagnostics (used by the parity tests): evaluate the device geometry kernels
  * on host arrays.  pts: n x 12 floats (x0,x1,x2,x3) -> out: n floats;
  * variant 0 = point_triangle_distance as used by the band kernel, 1 = the
- * branch-free form, 2 = the wave-uniform form used by the tile sweep (all three
- * must give identical bits).
+ * branch-free form, 2 = the wave-uniform form used by the tile sweep, 3/4 = the
+ * packed two-pair form (the first / second half of a pair of adjacent inputs);
+ * all must give identical bits.
  * pit: n x 8 doubles (x0,y0,x1,y1,x2,y2,x3,y3) -> out4: n x (flag,a,b,c). */
 int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, float *out,
                          char *errbuf, size_t errlen);

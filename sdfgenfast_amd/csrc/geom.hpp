@@ -168,6 +168,76 @@ __device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3)
     return r;
 }
 
+// Two point-triangle distances per lane in packed FP32 (v_pk_mul_f32 / v_pk_add_f32: each
+// half is an IEEE single operation with round-to-nearest, exactly the scalar op), so a lane
+// that owns two (cell, candidate) pairs evaluates both in one pass.  Division, sqrt, compares
+// and selects stay scalar per half.  Bit-identical to ptd_nb for each pair.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct f3x2 {
+    f2v x, y, z;
+};
+__device__ __forceinline__ f3x2 mk3x2(f3 a, f3 b) { return f3x2{f2v{a.x, b.x}, f2v{a.y, b.y}, f2v{a.z, b.z}}; }
+__device__ __forceinline__ f3x2 sub3x2(f3x2 a, f3x2 b) { return f3x2{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f2v mag2x2(f3x2 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+__device__ __forceinline__ f2v dot3x2(f3x2 a, f3x2 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
+__device__ __forceinline__ f2v sel2(bool c0, bool c1, f2v a, f2v b) { return f2v{c0 ? a.x : b.x, c1 ? a.y : b.y}; }
+__device__ __forceinline__ f3x2 sel3x2(bool c0, bool c1, f3x2 a, f3x2 b)
+{
+    return f3x2{sel2(c0, c1, a.x, b.x), sel2(c0, c1, a.y, b.y), sel2(c0, c1, a.z, b.z)};
+}
+__device__ __forceinline__ f2v sqrt2(f2v v) { return f2v{sqrt_rn(v.x), sqrt_rn(v.y)}; }
+__device__ __forceinline__ f2v dist3x2(f3x2 a, f3x2 b)
+{
+    const f3x2 d = sub3x2(a, b);
+    return sqrt2((d.x * d.x + d.y * d.y) + d.z * d.z);
+}
+__device__ __forceinline__ f2v psd2(f3x2 x0, f3x2 x1, f3x2 x2)
+{
+    const f3x2 e = sub3x2(x2, x1);
+    const f2v m2 = mag2x2(e);
+    const f3x2 t = sub3x2(x2, x0);
+    const f2v dt = dot3x2(t, e);
+    // (float)((double)dt / (double)m2) == the IEEE float division dt / m2
+    f2v s12 = f2v{(float)((double)dt.x / (double)m2.x), (float)((double)dt.y / (double)m2.y)};
+    s12.x = (s12.x < 0.0f) ? 0.0f : ((s12.x > 1.0f) ? 1.0f : s12.x);
+    s12.y = (s12.y < 0.0f) ? 0.0f : ((s12.y > 1.0f) ? 1.0f : s12.y);
+    const f2v w = 1.0f - s12;
+    const f3x2 p = f3x2{x1.x * s12 + x2.x * w, x1.y * s12 + x2.y * w, x1.z * s12 + x2.z * w};
+    return dist3x2(x0, p);
+}
+__device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, f3 x0b, f3 x1b, f3 x2b, f3 x3b, float &da,
+                                          float &db)
+{
+    const f3x2 x0 = mk3x2(x0a, x0b), x1 = mk3x2(x1a, x1b), x2 = mk3x2(x2a, x2b), x3 = mk3x2(x3a, x3b);
+    const f3x2 x13 = sub3x2(x1, x3), x23 = sub3x2(x2, x3), x03 = sub3x2(x0, x3);
+    const f2v m13 = mag2x2(x13), m23 = mag2x2(x23), d = dot3x2(x13, x23);
+    const f2v det = m13 * m23 - d * d;
+    const f2v invdet = f2v{div_rn(1.0f, fmax_std(det.x, 1e-30f)), div_rn(1.0f, fmax_std(det.y, 1e-30f))};
+    const f2v a = dot3x2(x13, x03), b = dot3x2(x23, x03);
+    const f2v w23 = invdet * (m23 * a - d * b);
+    const f2v w31 = invdet * (m13 * b - d * a);
+    const f2v w12 = (1.0f - w23) - w31;
+    const bool ia = (w23.x >= 0.0f) & (w31.x >= 0.0f) & (w12.x >= 0.0f);
+    const bool ib = (w23.y >= 0.0f) & (w31.y >= 0.0f) & (w12.y >= 0.0f);
+    f2v r = f2v{0.0f, 0.0f};
+    if (__any(ia | ib)) {
+        const f3x2 p = f3x2{(x1.x * w23 + x2.x * w31) + x3.x * w12, (x1.y * w23 + x2.y * w31) + x3.y * w12,
+                            (x1.z * w23 + x2.z * w31) + x3.z * w12};
+        r = dist3x2(x0, p);
+    }
+    if (__any(!ia | !ib)) {
+        const bool c23a = w23.x > 0.0f, c31a = !c23a & (w31.x > 0.0f);
+        const bool c23b = w23.y > 0.0f, c31b = !c23b & (w31.y > 0.0f);
+        const f3x2 fb = sel3x2(c23a | c31a, c23b | c31b, x2, x3);
+        const f3x2 sa = sel3x2(c23a, c23b, x1, x2);
+        const f2v first = psd2(x0, x1, fb), second = psd2(x0, sa, x3);
+        const f2v de = f2v{fmin_std(first.x, second.x), fmin_std(first.y, second.y)};
+        r = sel2(ia, ib, r, de);
+    }
+    da = r.x;
+    db = r.y;
+}
+
 // orientation (SOS-robust 2D), FP64.
 SDF_HD int orientation(double x1, double y1, double x2, double y2, double &area)
 {

@@ -350,6 +350,25 @@ __global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__
     const float *p = pts + 12 * q;
     const f3 x0 = mk3(p[0], p[1], p[2]), x1 = mk3(p[3], p[4], p[5]), x2 = mk3(p[6], p[7], p[8]),
              x3 = mk3(p[9], p[10], p[11]);
+    if (variant == 3) {   // packed pair: this lane's point against its own and its neighbour's triangle
+        const uint64_t q2 = (q ^ 1) < n ? (q ^ 1) : q;
+        const float *r = pts + 12 * q2;
+        float da, db;
+        ptd_wave2(x0, x1, x2, x3, x0, mk3(r[3], r[4], r[5]), mk3(r[6], r[7], r[8]), mk3(r[9], r[10], r[11]), da, db);
+        out[q] = da;
+        (void)db;
+        return;
+    }
+    if (variant == 4) {   // packed pair, second half: the neighbour's point against this lane's triangle
+        const uint64_t q2 = (q ^ 1) < n ? (q ^ 1) : q;
+        const float *r = pts + 12 * q2;
+        float da, db;
+        ptd_wave2(mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), mk3(r[6], r[7], r[8]), mk3(r[9], r[10], r[11]), x0,
+                  x1, x2, x3, da, db);
+        out[q] = db;
+        (void)da;
+        return;
+    }
     out[q] = variant == 0 ? ptd(x0, x1, x2, x3) : (variant == 1 ? ptd_nb(x0, x1, x2, x3) : ptd_wave(x0, x1, x2, x3));
 }
 

@@ -448,8 +448,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         const int l2 = p2 & 63, e2 = p2 >> 9;
                         const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
                                             c0 + ST_CLW * w + (l2 >> 3));
-                        const float d1 = ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
-                        const float d2 = ptd_wave(g2, st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]));
+                        float d1, d2;
+                        ptd_wave2(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]), g2,
+                                  st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]), d1, d2);
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
                         if (has2) s_d[w][((p2 >> 6) & 7) * ST_CPW + l2] = d2;
                     } else {

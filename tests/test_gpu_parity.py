@@ -43,7 +43,7 @@ def _ptd_inputs(n, seed):
     return pts
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_device_ptd_bitwise_vs_oracle(variant):
     pts = _ptd_inputs(4_000_000, 7)
     got = _lib.debug_ptd(pts, variant=variant)
