@@ -216,18 +216,21 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
         if (merge)
             for (unsigned c = tid; c < uvol; c += 256) s_key[c] = ~0ull;
         __syncthreads();
-        for (unsigned fl = tid; fl < total; fl += 256) {
-            int q = 0;   // triangle of flat index fl: last q with s_pre[q] <= fl
+        // (triangle, cell) pair of flat index fl
+        auto pair_of = [&](unsigned fl, int &i, int &j, int &k, uint64_t &t) {
+            int q = 0;   // last q with s_pre[q] <= fl
 #pragma unroll
             for (int step = BAND_BT / 2; step >= 1; step >>= 1)
                 if (q + step < nb && s_pre[q + step] <= fl) q += step;
             const BandBox B = s_box[q];
             const unsigned r = fl - s_pre[q], bij = (unsigned)(B.bi * B.bj);
             const unsigned kk = r / bij, rem = r - kk * bij, jj = rem / (unsigned)B.bi;
-            const int i = B.i0 + (int)(rem - jj * (unsigned)B.bi), j = B.j0 + (int)jj, k = B.k0 + (int)kk;
-            const uint64_t t = t0 + q;
-            const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
-            const float d = ptd(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2));
+            i = B.i0 + (int)(rem - jj * (unsigned)B.bi);
+            j = B.j0 + (int)jj;
+            k = B.k0 + (int)kk;
+            t = t0 + q;
+        };
+        auto emit = [&](float d, int i, int j, int k, uint64_t t) {
             if (d < init) {   // also rejects NaN
                 const u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
                 if (merge) {
@@ -237,6 +240,25 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
                     if (key < *p) atomicMin(p, key);
                 }
             }
+        };
+        // two pairs per lane (fl, fl + 256) evaluated together in packed FP32 (ptd_wave2)
+        for (unsigned fl = tid; fl < total; fl += 512) {
+            const bool two = fl + 256 < total;
+            int i, j, k, i2, j2, k2;
+            uint64_t t, t2;
+            pair_of(fl, i, j, k, t);
+            pair_of(two ? fl + 256 : fl, i2, j2, k2, t2);
+            const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
+            const f3 gx2 = mk3((float)i2 * g.dx + g.ox, (float)j2 * g.dx + g.oy, (float)k2 * g.dx + g.oz);
+            float d, d2 = 0.0f;
+            if (__any(two)) {
+                ptd_wave2(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2), gx2,
+                          load_vtx(soup, t2, 0), load_vtx(soup, t2, 1), load_vtx(soup, t2, 2), d, d2);
+            } else {
+                d = ptd_wave(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2));
+            }
+            emit(d, i, j, k, t);
+            if (two) emit(d2, i2, j2, k2, t2);
         }
         __syncthreads();
         if (merge)
