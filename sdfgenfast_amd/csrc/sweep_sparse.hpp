@@ -128,53 +128,48 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
     bool changed = false;
     const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
     const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
-    bool ev[7];
+    unsigned f = 0;   // candidates to evaluate, one bit per upwind slot q
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
         const int t = lab[q];
-        bool skip = (t < 0) || (t == ct0);
+        bool skip = (t < 0) | (t == ct0);
 #pragma unroll
-        for (int r = 0; r < q; ++r) skip = skip || (lab[r] == t);
-        skip = skip || (interior && lcq[q] <= P.seen[q]);   // seen[q] = -1: never
-        ev[q] = !skip;
+        for (int r = 0; r < q; ++r) skip = skip | (lab[r] == t);
+        skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
+        f |= (skip ? 0u : 1u) << q;
     }
-    if (LIVE) {
-        // The repair walks dependency chains one cell after another: issue every candidate's
-        // vertex gather at once (one memory round trip per cell, not one per candidate).
-        float4 v[7][3];
+    // Candidates in increasing q, two per pass in packed FP32 (ptd_wave2): every lane walks
+    // its own list, so a wave runs max(count)/2 passes instead of one divergent ptd per slot
+    // q that any lane needs.  Distances do not depend on phi, so applying each pair in q
+    // order right after it is evaluated is the reference's check order (:143-149).
+    while (__any(f != 0u)) {
+        const bool has_a = f != 0u;
+        const int qa = has_a ? __builtin_ctz(f) : 0;
+        f &= f - 1u;
+        const bool has_b = f != 0u;
+        const int qb = has_b ? __builtin_ctz(f) : qa;
+        f &= f - 1u;
+        int ta = lab[0], tb = lab[0];
 #pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            const size_t b = 3 * (size_t)(ev[q] ? lab[q] : 0);
-            v[q][0] = P.soup[b];
-            v[q][1] = P.soup[b + 1];
-            v[q][2] = P.soup[b + 2];
+        for (int q = 1; q < 7; ++q) {   // static indices: no register-array indexing
+            ta = (qa == q) ? lab[q] : ta;
+            tb = (qb == q) ? lab[q] : tb;
         }
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            if (ev[q]) {
-                const float d = ptd(gx, mk3(v[q][0].x, v[q][0].y, v[q][0].z), mk3(v[q][1].x, v[q][1].y, v[q][1].z),
-                                    mk3(v[q][2].x, v[q][2].y, v[q][2].z));
-                if (d < phi) {
-                    phi = d;
-                    ct = lab[q];
-                    changed = true;
-                }
-            }
+        const size_t ba = 3 * (size_t)(has_a ? ta : 0), bb = 3 * (size_t)(has_b ? tb : (has_a ? ta : 0));
+        const float4 a0 = P.soup[ba], a1 = P.soup[ba + 1], a2 = P.soup[ba + 2];
+        const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
+        float da, db;
+        ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), gx,
+                  mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), da, db);
+        if (has_a && da < phi) {
+            phi = da;
+            ct = ta;
+            changed = true;
         }
-    } else {
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-            if (ev[q]) {
-                const int t = lab[q];
-                const float4 v0 = P.soup[3 * (size_t)t], v1 = P.soup[3 * (size_t)t + 1],
-                             v2 = P.soup[3 * (size_t)t + 2];
-                const float d = ptd(gx, mk3(v0.x, v0.y, v0.z), mk3(v1.x, v1.y, v1.z), mk3(v2.x, v2.y, v2.z));
-                if (d < phi) {
-                    phi = d;
-                    ct = t;
-                    changed = true;
-                }
-            }
+        if (has_b && db < phi) {
+            phi = db;
+            ct = tb;
+            changed = true;
         }
     }
     if (!changed) return own;
