@@ -22,8 +22,9 @@ single-GPU C4 run, the reference point of the Z-slab efficiency.
 
 Rank 0 prints one JSON line with the driver's contract fields plus `roofline`
 (dominant kernel = the tile-wavefront sweep, HIP-event timed inside the library
-on the launch stream) and `cpu_baseline` (the oracle, 1 thread, on a bounded
-sample; N=1 only).
+on the launch stream) and `cpu_baseline` (N=1 only: the reference's own CPU path,
+multi-threaded on this host, on the full workload; the oracle on a sample when the
+reference build is absent).
 """
 import argparse
 import hashlib
@@ -49,12 +50,38 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _host_threads() -> int:
+    """Host cores this job may use: the box's CPU share (OMP_NUM_THREADS is set to it on the
+    GPU boxes; os.cpu_count() there shows the whole machine), else the affinity set."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return max(1, min(len(os.sched_getaffinity(0)), 16))
+    except AttributeError:
+        return max(1, min(os.cpu_count() or 1, 16))
+
+
 def cpu_baseline(workload: str):
-    """Oracle (oracle/sdf_oracle.c, 1 thread) on a bounded sample: the same 1M-triangle
-    mesh on a 128^3 grid (same mode-2b recipe) -- about 6 s of CPU work."""
+    """The reference's own CPU path (cpu_lib/makelevelset3.cpp compiled from /root/reference into
+    oracle/_ref/ by `make -C oracle ref`; the built .so travels with the tree) with its
+    multi-threaded sweep on this host's cores, on the FULL workload -- about 10 s.  Its k-split
+    sweep races, so this is a timing baseline only.  Without oracle/_ref: the C
+    restatement (oracle/sdf_oracle.c, 1 thread) on a bounded sample (same mesh at 128^3)."""
     from oracle import oracle as O
     from sdfgenfast_amd import meshgen
 
+    if O.ref_available():
+        v, t, o, dx, dims = meshgen.workload(workload)
+        th = _host_threads()
+        t0 = time.perf_counter()
+        O.ref_make_level_set3(v, t, o, dx, *dims, 1, num_threads=th)
+        el = time.perf_counter() - t0
+        n = dims[0] * dims[1] * dims[2]
+        return {"value": round(n / el / 1e6, 4), "unit": "Mvoxels/s", "cores": th, "kind": "reference",
+                "sample": f"reference cpu_lib make_level_set3 (oracle/_ref), num_threads={th}, the full "
+                          f"{workload} workload ({n} voxels, {t.shape[0]} triangles), {el:.2f} s; 1 thread: "
+                          f"see tests/golden/hashes.json ref_seconds_1thread"}
     w = meshgen.WORKLOADS[workload]
     v, t = meshgen.bumpy_sphere(w["nu"], w["nv"])
     n = 128

@@ -150,7 +150,8 @@ def ref_pit2d_batch(pit: np.ndarray) -> np.ndarray:
 
 
 def ref_make_level_set3(vertices, triangles, origin, dx, ni, nj, nk, exact_band=1, num_threads=1):
-    """The REFERENCE implementation (development container only)."""
+    """The REFERENCE implementation (built in the development container; bench.py's
+    cpu_baseline also times it, multi-threaded, on the GPU box)."""
     v, t, o = _prep(vertices, triangles, origin)
     out = np.empty(ni * nj * nk, dtype=np.float32)
     ref_lib().ref_make_level_set3(_ptr(t), t.shape[0], _ptr(v), v.shape[0], _ptr(o), ctypes.c_float(dx),

@@ -1,7 +1,9 @@
 // oracle/ref_shim.cpp -- extern "C" wrapper around the REFERENCE CPU implementation.
 //
-// TEST INFRASTRUCTURE ONLY, built only in the development container (never on
-// the GPU box, where /root/reference does not exist): oracle/Makefile compiles
+// TEST INFRASTRUCTURE ONLY, built only in the development container (the GPU box
+// has no /root/reference; the built .so travels with the tree and bench.py's
+// cpu_baseline leg times it there -- the reference's multi-threaded CPU path, a
+// timing baseline, never a checker of GPU results on the box): oracle/Makefile compiles
 // the reference's own cpu_lib/makelevelset3.cpp where it lies under
 // /root/reference (it is #included below so that its file-static helpers
 // point_triangle_distance / point_in_triangle_2d are reachable) with the

@@ -27,7 +27,8 @@ for J in range(nJ):
     s0, s1, s2, s3 = st[q]
     lag = f"{s1 - prev:6.1f}" if prev is not None else "     -"
     print(f"  ({J:2d},{J:2d}) start {s0:8.1f} first {s1:8.1f} (+{lag}) end {s3:8.1f}  dur {s3 - s1:7.1f} "
-          f"us/step {(s3 - s1) / nsteps:5.2f} wait {tr[q, 4] / 100:7.1f} compute/step {tr[q, 7] / 100.0 / nsteps:5.2f}")
+          f"us/step {(s3 - s1) / nsteps:5.2f} wait {tr[q, 4] / 100:7.1f} compute/step {tr[q, 7] / 100.0 / nsteps:5.2f} "
+          f"waits own/other {tr[q, 5] & 0xffffffff}/{tr[q, 5] >> 32}")
     prev = s1
 # concurrency profile: number of tasks between first and end over time
 ts = np.linspace(0, st[:, 3].max(), 12)
