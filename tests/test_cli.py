@@ -94,3 +94,50 @@ def test_cli_reproduces_reference_sdf_file_gpu(x3y4z5_stl, tmp_path):
     assert "GPU (HIP" in r.stdout
     out = tmp_path / "test_x3y4z5_bin_sdf_32x32x32.sdf"
     assert hashlib.sha256(out.read_bytes()).hexdigest() == REF_SHA
+
+
+def test_cli_mode2a_proportional_dims_and_header(x3y4z5_stl, tmp_path):
+    """tests/test_cli_modes.cpp:94-100: `Nx=32` on the x3y4z5 mesh -> a 32x42x52 grid,
+    named <base>_sdf_32x42x52.sdf, header dims match; values = the prop32 fixture."""
+    p, _ = x3y4z5_stl
+    r = _run(["--backend", "cpu", "-q", p.name, "32"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    out = tmp_path / "test_x3y4z5_bin_sdf_32x42x52.sdf"
+    raw = out.read_bytes()
+    assert struct.unpack("<3i", raw[:12]) == (32, 42, 52)
+    c = next(g for g in GOLDEN_CASES if g.name == "x3y4z5_stl_prop32")
+    got = np.frombuffer(raw[36:], dtype="<f4").reshape(32, 42, 52)
+    assert np.array_equal(got.view(np.uint32), np.ascontiguousarray(c.phi, np.float32).view(np.uint32))
+    mn = struct.unpack("<3f", raw[12:24])
+    assert np.allclose(mn, c.origin)
+
+
+def test_cli_mode1_obj(tmp_path):
+    """Mode 1 (legacy OBJ + dx + padding): <base>.sdf, sizes = padded box / dx (truncated)."""
+    v, t = meshgen.bumpy_sphere(30, 11)
+    obj = tmp_path / "sphere.obj"
+    with open(obj, "w") as f:
+        for x in v:
+            f.write(f"v {x[0]:.9g} {x[1]:.9g} {x[2]:.9g}\n")
+        for tri in t:
+            f.write(f"f {tri[0] + 1} {tri[1] + 1} {tri[2] + 1}\n")
+    r = _run(["--backend", "cpu", "-q", obj.name, "0.1", "2"], tmp_path)
+    assert r.returncode == 0, r.stderr
+    raw = (tmp_path / "sphere.sdf").read_bytes()
+    dims = struct.unpack("<3i", raw[:12])
+    from sdfgenfast_amd import meshio
+    _, _, (mn, mx) = meshio.load_mesh(str(obj))
+    o, dx, want = cli.grid(cli.plan([obj.name, "0.1", "2"]), mn, mx)
+    assert dims == want and len(raw) == 36 + 4 * int(np.prod(dims))
+    phi = np.frombuffer(raw[36:], dtype="<f4").reshape(dims)
+    assert phi[dims[0] // 2, dims[1] // 2, dims[2] // 2] < 0 and phi[0, 0, 0] > 0
+
+
+def test_cli_errors(tmp_path):
+    """test_cli_errors: usage text for too few arguments, failure for a missing mesh."""
+    r = _run([], tmp_path)
+    assert r.returncode != 0 and "mode 1" in (r.stdout + r.stderr).lower()
+    r = _run(["--backend", "cpu", "missing.stl", "32"], tmp_path)
+    assert r.returncode != 0 and "Failed to load mesh" in r.stderr
+    r = _run(["--backend", "cpu", "m.stl", "0"], tmp_path)
+    assert r.returncode != 0
