@@ -101,6 +101,16 @@ __device__ __forceinline__ unsigned long long st_granule(unsigned epoch, uint32_
 }
 __device__ __forceinline__ bool st_granule_ready(unsigned long long g, unsigned epoch) { return (uint32_t)(g >> 32) == epoch; }
 
+// Per-sweep fields of one launch that runs several sweeps (MULTI, see k_sweep_tile).
+constexpr int ST_MAXSW = 8;
+constexpr int ST_MAXDEP = 16;   // previous-sweep tiles a tile depends on (3x3 with margins)
+struct StSweep {
+    unsigned long long *hb, *hc;  // this sweep's halo granule buffers
+    int di, dj, dk, sweep;
+    unsigned epoch;
+    int seen[7];
+};
+
 struct StParams {
     const float4 *soup;           // 3 float4 per triangle (xyz; w unused)
     unsigned long long *cell;     // (phi bits << 32) | closest_tri, i-fastest
@@ -127,6 +137,12 @@ struct StParams {
     unsigned long long *hc_out;
     int seen[7];   // per upwind slot q: s'+1 of the last earlier sweep in which an interior cell
                    // examined that neighbour (-1: none) -- see sweep_sparse.hpp
+    // MULTI: tasks of ST_MAXSW consecutive sweeps in one launch (cross-sweep overlap)
+    const int4 *mtasks;           // (J, K, sweep slot, -) in dequeue order
+    const int *deps;              // [task][ST_MAXDEP]: earlier tasks (previous sweep) to wait for, -1 = none
+    unsigned *done;               // [task] = call_epoch once the task's cell stores are visible
+    unsigned call_epoch;
+    StSweep sw[ST_MAXSW];
 };
 
 __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
@@ -205,9 +221,13 @@ __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v
 // SLAB: halo granules may come from another GPU (IPC-mapped inbox), so granule loads
 // and stores are made at system scope; the single-GPU build keeps agent scope.
 // TRACE: per-task timestamps for tools/trace_diag.py (kept out of the normal build's loop).
-template <bool SLAB, bool TRACE>
-__global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams P)
+// MULTI: one launch runs the tasks of several consecutive sweeps (the first pass), each task
+// first waiting for the tiles of the previous sweep whose cells it reads or overwrites; the
+// task order is topological, so every awaited tile is already claimed.
+template <bool SLAB, bool TRACE, bool MULTI = false>
+__global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams P0)
 {
+    StParams P = P0;
     constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
     __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
@@ -242,8 +262,45 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         __syncthreads();
         const int task = s_task;
         if (task >= P.ntasks) break;
-        const int2 JK = P.tasks[task];
-        const int J = JK.x, K = JK.y;
+        int J, K;
+        if (MULTI) {
+            const int4 tk = P0.mtasks[task];
+            J = tk.x;
+            K = tk.y;
+            const StSweep &sw = P0.sw[tk.z];
+            P.hb = sw.hb;
+            P.hc = sw.hc;
+            P.di = sw.di;
+            P.dj = sw.dj;
+            P.dk = sw.dk;
+            P.sweep = sw.sweep;
+            P.epoch = sw.epoch;
+#pragma unroll
+            for (int q = 0; q < 7; ++q) P.seen[q] = sw.seen[q];
+            if (wave == 0) {
+                // the previous sweep's tiles under and around this one: their cell stores first
+                const int dep = L < ST_MAXDEP ? P0.deps[(size_t)task * ST_MAXDEP + L] : -1;
+                bool ok = dep < 0;
+                for (unsigned spins = 0;; ++spins) {
+                    if (!ok) ok = __hip_atomic_load(P0.done + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                                  P0.call_epoch;
+                    if (__all(ok)) break;
+                    if (spins > ST_WATCHDOG || ((spins & 255u) == 255u && st_failed(P))) {
+                        if (L == 0) st_fail(P, 8);
+                        break;
+                    }
+                    if (spins < 16) __builtin_amdgcn_s_sleep(1);
+                    else __builtin_amdgcn_s_sleep(8);
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // this CU reads them fresh
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            __syncthreads();
+        } else {
+            const int2 JK = P.tasks[task];
+            J = JK.x;
+            K = JK.y;
+        }
         const int b0 = J * ST_T, c0 = P.cs + K * ST_T;
         const bool inbox = SLAB && K == 0 && P.hc_in != nullptr;   // c0-1 lives on the upstream GPU
         const int nsteps = P.A + 2 * (ST_T - 1);
@@ -689,7 +746,13 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 }
             }
         }
+        if (MULTI) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's cell stores done
         __syncthreads();
+        if (MULTI && tid == 0) {   // ... then one release and the flag (MI355X_MICROARCH.md visibility)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(P0.done + task, P0.call_epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     if (P.stats && L == 0) {
         if (n_evals) atomicAdd(P.stats, n_evals);
@@ -721,6 +784,15 @@ struct TileSweepWorkspace {
     int *ctrl = nullptr;   // [0] queue counter, [1] error bits
     unsigned epoch = 0;
     bool count = false;
+    // MULTI launches (tile_sweep_multi): per-sweep halo buffers, task graph, completion flags
+    unsigned long long *mhb = nullptr, *mhc = nullptr;
+    size_t cap_mhb = 0, cap_mhc = 0;
+    int4 *mtasks = nullptr;
+    int *mdeps = nullptr;
+    unsigned *mdone = nullptr;
+    size_t cap_mtasks = 0;
+    long long mkey = -1;   // (ni, nj, nk, first sweep, count) of the uploaded graph
+    unsigned mepoch = 0;
 };
 
 inline bool tile_sweep_supported(int ni, int nj, int nk) { return ni >= 2 && nj >= 2 && nk >= 2; }
@@ -863,8 +935,182 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     return 0;
 }
 
+// Physical (j or k) index range of oriented tile T along an axis of n cells swept in direction d.
+inline void st_tile_range(int T, int n, int d, int *lo, int *hi)
+{
+    const int bl = ST_T * T, bh = std::min(ST_T * T + ST_T - 1, n - 2);   // oriented b in [0, n-1)
+    if (d > 0) { *lo = bl + 1; *hi = bh + 1; }
+    else { *lo = n - 2 - bh; *hi = n - 2 - bl; }
+}
+
+// Sweeps s0 .. s0+ns-1 (first pass) in ONE persistent launch: the tasks of all of them in a
+// topological order by an estimated start time, so a sweep's first tiles start while the
+// previous sweep's last tiles still run.  Each task waits for the tiles of
+// the previous sweep that cover its columns (one cell of margin on every side: the face
+// cells it reads and the cells a neighbour tile of the previous sweep reads).
+inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
+                            const float origin[3], float dx, int ni, int nj, int nk, int s0, int ns,
+                            const int (*dirs)[3], char *err, size_t errlen)
+{
+    const int A = ni - 1, B = nj - 1, C = nk - 1;
+    const int nJ = (B + ST_T - 1) / ST_T, nK = (C + ST_T - 1) / ST_T;
+    const int per = nJ * nK, ntasks = ns * per;
+    auto fail = [&](int code, const char *msg) {
+        if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
+        return code;
+    };
+    if (ns < 1 || ns > ST_MAXSW || per <= 0) return fail(-1, "bad multi-sweep request");
+    const size_t nhb = (size_t)nJ * C * A, nhc = (size_t)nK * B * A;
+    if (W.cap_mhb < ns * nhb || W.cap_mhc < ns * nhc) (void)hipStreamSynchronize(st);
+    if (st_grow(&W.mhb, &W.cap_mhb, ns * nhb)) return fail(-5, "halo buffer allocation failed");
+    if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc)) return fail(-5, "halo buffer allocation failed");
+    if (!W.ctrl) {
+        if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
+        if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
+        if (hipMemset(W.ctrl, 0, 16 * sizeof(int)) != hipSuccess) return fail(-4, "memset");
+    }
+    const long long key = ((((long long)ni * 65536 + nj) * 65536 + nk) * 64 + s0) * 16 + ns;
+    if (W.mkey != key) {
+        (void)hipStreamSynchronize(st);   // the tables may still be read by a running launch
+        // ranges of every tile of every sweep, then estimated starts (in units of one tile hop
+        // = ST_T steps): +1 per upstream tile of the same sweep, + the tile duration after
+        // each previous-sweep tile it waits for
+        const double wc = (A + 2.0 * (ST_T - 1)) / ST_T;
+        std::vector<double> key_est((size_t)ntasks, 0.0);
+        std::vector<std::vector<int>> dep((size_t)ntasks);
+        auto id = [&](int q, int J, int K) { return (q * nJ + J) * nK + K; };
+        for (int q = 0; q < ns; ++q) {
+            const int *d = dirs[(s0 + q) % 8], *dp = dirs[(s0 + q + 7) % 8];
+            for (int J = 0; J < nJ; ++J)
+                for (int K = 0; K < nK; ++K) {
+                    double kv = 0.0;
+                    if (J) kv = std::max(kv, key_est[id(q, J - 1, K)] + 1.0);
+                    if (K) kv = std::max(kv, key_est[id(q, J, K - 1)] + 1.0);
+                    if (q) {
+                        int jl, jh, kl, kh;
+                        st_tile_range(J, nj, d[1], &jl, &jh);
+                        st_tile_range(K, nk, d[2], &kl, &kh);
+                        --jl; ++jh; --kl; ++kh;
+                        for (int J2 = 0; J2 < nJ; ++J2) {
+                            int a0, a1;
+                            st_tile_range(J2, nj, dp[1], &a0, &a1);
+                            if (a1 < jl || a0 > jh) continue;
+                            for (int K2 = 0; K2 < nK; ++K2) {
+                                int c0, c1;
+                                st_tile_range(K2, nk, dp[2], &c0, &c1);
+                                if (c1 < kl || c0 > kh) continue;
+                                dep[id(q, J, K)].push_back(id(q - 1, J2, K2));
+                                kv = std::max(kv, key_est[id(q - 1, J2, K2)] + wc);
+                            }
+                        }
+                        if (dep[id(q, J, K)].size() > (size_t)ST_MAXDEP) return fail(-1, "tile dependency overflow");
+                    }
+                    key_est[id(q, J, K)] = kv;
+                }
+        }
+        std::vector<int> order((size_t)ntasks);
+        for (int t = 0; t < ntasks; ++t) order[t] = t;
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key_est[x] < key_est[y]; });
+        std::vector<int> pos((size_t)ntasks);
+        for (int r = 0; r < ntasks; ++r) pos[order[r]] = r;
+        std::vector<int4> mt((size_t)ntasks);
+        std::vector<int> md((size_t)ntasks * ST_MAXDEP, -1);
+        for (int r = 0; r < ntasks; ++r) {
+            const int t = order[r], q = t / per, J = (t % per) / nK, K = t % nK;
+            mt[r] = make_int4(J, K, q, 0);
+            int m = 0;
+            for (int u : dep[t]) {
+                if (pos[u] >= r) return fail(-1, "tile order not topological");
+                md[(size_t)r * ST_MAXDEP + m++] = pos[u];
+            }
+        }
+        if (W.cap_mtasks < (size_t)ntasks) {
+            (void)hipFree(W.mtasks);
+            (void)hipFree(W.mdeps);
+            (void)hipFree(W.mdone);
+            W.mtasks = nullptr;
+            W.mdeps = nullptr;
+            W.mdone = nullptr;
+            W.cap_mtasks = 0;
+            if (hipMalloc((void **)&W.mtasks, ntasks * sizeof(int4)) != hipSuccess ||
+                hipMalloc((void **)&W.mdeps, (size_t)ntasks * ST_MAXDEP * sizeof(int)) != hipSuccess ||
+                hipMalloc((void **)&W.mdone, ntasks * sizeof(unsigned)) != hipSuccess)
+                return fail(-5, "task graph allocation failed");
+            if (hipMemset(W.mdone, 0, ntasks * sizeof(unsigned)) != hipSuccess) return fail(-4, "memset");
+            W.cap_mtasks = ntasks;
+        }
+        if (hipMemcpy(W.mtasks, mt.data(), ntasks * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(W.mdeps, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+            return fail(-4, "task graph upload");
+        W.mkey = key;
+    }
+    if (++W.mepoch == 0) ++W.mepoch;   // completion flags of this launch (0 = never)
+    if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+    StParams P;
+    memset(&P, 0, sizeof(P));
+    P.soup = soup;
+    P.cell = cell;
+    P.queue = W.ctrl;
+    P.err = W.ctrl + 1;
+    P.stats = W.count ? W.stats : nullptr;
+    P.trace = nullptr;
+    P.ox = origin[0];
+    P.oy = origin[1];
+    P.oz = origin[2];
+    P.dx = dx;
+    P.ni = ni;
+    P.nj = nj;
+    P.nk = nk;
+    P.A = A;
+    P.B = B;
+    P.C = C;
+    P.nJ = nJ;
+    P.nK = nK;
+    P.ntasks = ntasks;
+    P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
+    P.cs = 0;
+    P.ce = C;
+    P.mtasks = W.mtasks;
+    P.deps = W.mdeps;
+    P.done = W.mdone;
+    P.call_epoch = W.mepoch;
+    for (int q = 0; q < ns; ++q) {
+        const int sw = s0 + q, *d = dirs[sw % 8];
+        StSweep &S = P.sw[q];
+        S.hb = W.mhb + q * nhb;
+        S.hc = W.mhc + q * nhc;
+        S.di = d[0];
+        S.dj = d[1];
+        S.dk = d[2];
+        S.sweep = sw;
+        if (++W.epoch == 0) ++W.epoch;
+        S.epoch = W.epoch;
+        for (int qq = 0; qq < 7; ++qq) {   // the "already examined" rule, as in tile_sweep
+            const int m = qq + 1;
+            S.seen[qq] = -1;
+            for (int s2 = sw - 1; s2 >= 0 && W.skip_seen; --s2) {
+                const int *e = dirs[s2 % 8];
+                if ((!(m & 1) || e[0] == d[0]) && (!(m & 2) || e[1] == d[1]) && (!(m & 4) || e[2] == d[2])) {
+                    S.seen[qq] = s2 + 1;
+                    break;
+                }
+            }
+        }
+    }
+    int grid = ntasks < 2048 ? ntasks : 2048;
+    if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
+    hipLaunchKernelGGL((k_sweep_tile<false, false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
+    return 0;
+}
+
 inline void tile_sweep_release(TileSweepWorkspace &W)
 {
+    (void)hipFree(W.mhb);
+    (void)hipFree(W.mhc);
+    (void)hipFree(W.mtasks);
+    (void)hipFree(W.mdeps);
+    (void)hipFree(W.mdone);
     (void)hipFree(W.hb);
     (void)hipFree(W.hc);
     (void)hipFree(W.tasks[0]);

@@ -1,0 +1,27 @@
+"""A/B by environment: python tools/ab_env.py WORKLOAD 'VAR=a' 'VAR=b' ... (each in a subprocess, interleaved)."""
+import json, os, subprocess, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+wl, cfgs = sys.argv[1], sys.argv[2:]
+code = r'''
+import sys, json; sys.path.insert(0, %r)
+from sdfgenfast_amd import _lib, meshgen
+v, t, o, dx, dims = meshgen.workload(%r)
+best = None
+for rep in range(6):
+    _lib.make_level_set3(v, t, o, dx, *dims, 1)
+    p = _lib.last_profile()
+    if rep and (best is None or p["total_ms"] < best["total_ms"]): best = p
+print(json.dumps({k: best[k] for k in ("total_ms", "band_ms", "sweep_ms")} | {"sw": [round(x, 3) for x in best["sweep_launch_ms"]]}))
+''' % (ROOT, wl)
+for rnd in range(2):
+    for cfg in cfgs:
+        env = dict(os.environ)
+        for kv in cfg.split(","):
+            if "=" in kv:
+                k, v = kv.split("=", 1)
+                env[k] = v
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+        if r.returncode:
+            print(cfg, "FAILED", r.stderr[-800:]); sys.exit(1)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        print(f"{cfg:28s} total {d['total_ms']:7.3f} band {d['band_ms']:6.3f} sweep {d['sweep_ms']:7.3f} | tile {sum(d['sw'][:8]):6.3f} sparse {sum(d['sw'][8:]):6.3f}", flush=True)
