@@ -154,8 +154,11 @@ def measure(workload, mode, steps, warmup, dev, dist, world, rank, verify=True):
     n_tile = last["sparse_first"] if last["sparse_sweeps"] else 16
     A, B, C = ni - 1, nj - 1, nk - 1
     tile_ms = [sum(p["sweep_launch_ms"][s] for p in profs) / len(profs) for s in range(n_tile)]
-    launch_ms = sum(tile_ms) / max(len(tile_ms), 1)
-    bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * C
+    multi = last.get("tile_multi", 0)   # the first pass as one overlapped launch of `multi` sweeps
+    launches = 1 if multi > 1 else max(len(tile_ms), 1)
+    launch_ms = sum(tile_ms) / launches
+    sweeps_per_launch = multi if multi > 1 else 1
+    bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * C * sweeps_per_launch
     if sess is not None:   # this rank's slab; the slab sessions run all 16 sweeps as tile wavefronts
         bytes_per_launch = SWEEP_BYTES_PER_CELL * A * B * (sess.k_end - sess.k_begin)
     sparse_ms = [sum(p["sweep_launch_ms"][s] for p in profs) / len(profs) for s in range(n_tile, 16)]
@@ -163,8 +166,8 @@ def measure(workload, mode, steps, warmup, dev, dist, world, rank, verify=True):
               for k in ("prep_ms", "band_ms", "sweep_ms", "sign_ms", "total_ms")}
     phases["tile_sweeps_ms"] = round(sum(tile_ms), 4)
     phases["sparse_sweeps_ms"] = round(sum(sparse_ms), 4)
-    r.update(n_tile=n_tile, launch_ms=launch_ms, bytes_per_launch=bytes_per_launch, phases=phases,
-             sweep_impl=last["sweep_impl"])
+    r.update(n_tile=launches, launch_ms=launch_ms, bytes_per_launch=bytes_per_launch, phases=phases,
+             sweep_impl=last["sweep_impl"], sweeps_per_launch=sweeps_per_launch)
 
     r["parity"] = None
     if verify:
@@ -305,6 +308,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                          "traffic_source": traffic_src, "kernel": "k_sweep_tile",
+                         "sweeps_per_launch": r["sweeps_per_launch"],
                          "launches_per_step": r["n_tile"], "avg_launch_ms": round(r["launch_ms"], 5),
                          "algorithmic_bytes_per_launch": int(r["bytes_per_launch"])},
             "phases_ms": r["phases"],

@@ -112,6 +112,9 @@ typedef struct sdfgen_hip_profile {
     int sparse_first;         /* index of the first such sweep (16 = none) */
     uint64_t sparse_rechecks; /* cell re-evaluations in the repair kernels (all sparse sweeps) */
     uint64_t sparse_claims;   /* rechecks run depth-first by the lane that requested them */
+    int tile_multi;           /* first-pass sweeps run as ONE overlapped launch (0: one launch per
+                                 sweep); its time is then sweep_launch_ms[0] */
+    int reserved_;
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

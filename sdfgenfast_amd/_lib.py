@@ -72,6 +72,8 @@ class Profile(ctypes.Structure):
         ("sparse_first", ctypes.c_int),
         ("sparse_rechecks", ctypes.c_uint64),
         ("sparse_claims", ctypes.c_uint64),
+        ("tile_multi", ctypes.c_int),
+        ("reserved_", ctypes.c_int),
     ]
 
     def as_dict(self):

@@ -665,6 +665,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.helper_polls = wf_stats[2];
     p.own_waits = wf_stats[3];
     p.sparse_sweeps = sparse_sweeps;
+    p.tile_multi = multi_n;
     p.sparse_first = sparse_sweeps ? sparse_first : 16;
     p.sparse_rechecks = sp_ctl[SP_RUNS];
     p.sparse_claims = sp_ctl[SP_ENQ];
