@@ -667,6 +667,10 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sparse_sweeps = sparse_sweeps;
     p.tile_multi = multi_n;
     p.sparse_first = sparse_sweeps ? sparse_first : 16;
+#ifdef SP_JACOBI_COUNT
+    fprintf(stderr, "jacobi candidates %llu lane-passes %llu (slot use %.3f)\n", sp_ctl[SP_DIAG], sp_ctl[SP_DIAG + 1],
+            sp_ctl[SP_DIAG + 1] ? sp_ctl[SP_DIAG] / (2.0 * sp_ctl[SP_DIAG + 1]) : 0.0);
+#endif
     p.sparse_rechecks = sp_ctl[SP_RUNS];
     p.sparse_claims = sp_ctl[SP_ENQ];
     if (sparse_sweeps) p.sweep_impl = 2;
@@ -675,6 +679,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         g_prof = p;
     }
     if (wf_err) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
+    if (sp_ctl[SP_ERR] & 4ull) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sparse sweep: Jacobi list overflow");
     if (sp_ctl[SP_ERR]) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sparse sweep watchdog fired (work list stalled)");
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
                              (unsigned long long)nvert);

@@ -41,7 +41,12 @@ namespace sdfhip {
 
 // ctl[SP_QUEUE]: work items appended to the ring (low 32 bits) and work items queued or
 // running (high 32 bits) in ONE word, so an append is one atomic round trip.
-enum { SP_QUEUE = 0, SP_HEAD = 1, SP_ERR = 3, SP_ENQ = 4, SP_RUNS = 5, SP_NCTL = 8 };
+// ctl layout: words 0..7 accumulate over the call (error bits, statistics); from SP_QUEUE
+// on everything is reset before each sweep: the work-list counters, then the Jacobi list
+// counters of SP_JPARTS parts, one 128-byte line each (a shared line serialises the
+// atomics of the whole grid: 1.4 ms per sweep at 256^3, measured).
+enum { SP_ERR = 0, SP_ENQ = 1, SP_RUNS = 2, SP_DIAG = 4, SP_QUEUE = 8, SP_HEAD = 9,
+       SP_JPARTS = 64, SP_JSTRIDE = 16, SP_JLIST = 16, SP_NCTL = SP_JLIST + SP_JPARTS * SP_JSTRIDE };
 constexpr unsigned long long SP_PENDING_ONE = 1ull << 32;
 constexpr unsigned long long SP_TAIL_LIMIT = 0xF0000000ull;   // appends per sweep (error beyond)
 constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
@@ -58,6 +63,8 @@ struct SpParams {
     unsigned long long *X;             // result of the sweep
     unsigned *req;                     // per-cell recheck requests (zero between sweeps)
     unsigned *queue;                   // ring of cell+1 (0 = empty)
+    unsigned *jlist;                   // Jacobi list: SP_JPARTS parts of jcap cells
+    unsigned long long jcap;
     unsigned long long *ctl;           // SP_* counters
     unsigned long long cap;            // ring slots
     unsigned long long n;              // cells
@@ -109,24 +116,20 @@ __device__ __forceinline__ bool sp_in(const SpParams &P, int i, int j, int k)
 // already seen that label.  A label set in this very sweep carries this sweep's stamp,
 // so the LIVE (repair) evaluation needs no extra check.
 template <bool LIVE>
-__device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
-                                                      int k, size_t c, unsigned long long own)
+__device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned long long *L, int i, int j, int k,
+                                            size_t c, unsigned long long own, int (&lab)[7])
 {
     const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
     const long long cc = (long long)c;
     const long long nb[7] = {cc - si, cc - sj, cc - si - sj, cc - sk, cc - si - sk, cc - sj - sk, cc - si - sj - sk};
-    int lab[7], lcq[7];
+    int lcq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
         const uint32_t w = (uint32_t)(LIVE ? sp_ld64(L + nb[q]) : L[nb[q]]);
         lab[q] = lbl_of(w);
         lcq[q] = lc_of(w);
     }
-    float phi = __uint_as_float((uint32_t)(own >> 32));
-    int ct = lbl_of((uint32_t)own);
-    const int ct0 = ct;
-    bool changed = false;
-    const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
+    const int ct0 = lbl_of((uint32_t)own);
     const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
     unsigned f = 0;   // candidates to evaluate, one bit per upwind slot q
 #pragma unroll
@@ -138,11 +141,34 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
         skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
         f |= (skip ? 0u : 1u) << q;
     }
+#ifdef SP_JACOBI_NOEVAL   // diagnostics only: the Jacobi pass's memory floor (wrong results)
+    if (!LIVE) f = 0;
+#endif
+    return f;
+}
+
+template <bool LIVE>
+__device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
+                                                      int k, size_t c, unsigned long long own)
+{
+    int lab[7];
+    unsigned f = sp_mask<LIVE>(P, L, i, j, k, c, own, lab);
+    float phi = __uint_as_float((uint32_t)(own >> 32));
+    int ct = lbl_of((uint32_t)own);
+    bool changed = false;
+    const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
+#ifdef SP_JACOBI_COUNT   // diagnostics only: candidates vs. packed slots the wave runs
+    unsigned passes_ = 0;
+    const unsigned cands_ = __builtin_popcount(f);
+#endif
     // Candidates in increasing q, two per pass in packed FP32 (ptd_wave2): every lane walks
     // its own list, so a wave runs max(count)/2 passes instead of one divergent ptd per slot
     // q that any lane needs.  Distances do not depend on phi, so applying each pair in q
     // order right after it is evaluated is the reference's check order (:143-149).
     while (__any(f != 0u)) {
+#ifdef SP_JACOBI_COUNT
+        ++passes_;
+#endif
         const bool has_a = f != 0u;
         const int qa = has_a ? __builtin_ctz(f) : 0;
         f &= f - 1u;
@@ -172,6 +198,12 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
             changed = true;
         }
     }
+#ifdef SP_JACOBI_COUNT
+    if (!LIVE) {
+        atomicAdd(&P.ctl[SP_DIAG], (unsigned long long)cands_);
+        atomicAdd(&P.ctl[SP_DIAG + 1], (unsigned long long)passes_);
+    }
+#endif
     if (!changed) return own;
     return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
 }
@@ -219,32 +251,99 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
     return mine;
 }
 
-// Pass 1 of the sparse sweep: every cell against the labels of S.
+// Pass 1 of the sparse sweep: every cell against the labels of S, in two kernels.
+// k_sp_jacobi streams the grid: a cell with no label left to examine (sp_mask == 0,
+// ~90 % of them) is copied to X as is; the others are appended to a compact list that
+// k_sp_jlist evaluates.  Evaluating in place would cost every wave as many ptd passes as
+// its busiest lane needs while ~7 % of the packed lanes carry a candidate (measured,
+// DESIGN.md §4); over the list nearly every lane has work.  Each wave gathers its list
+// cells in LDS and appends them with one atomic per ~200 cells.
+constexpr int SP_JWAVE = 256;   // LDS list entries per wave
+
+__device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32)
+{
+    const int i = (int)(c32 % (unsigned)P.ni);
+    const unsigned r = c32 / (unsigned)P.ni;
+    const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
+    const unsigned long long s = P.S[c32];
+    const unsigned long long y = sp_eval<false>(P, P.S, i, j, k, c32, s);
+    P.X[c32] = y;
+    if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) sp_request_downstream(P, i, j, k, c32, false);
+}
+
+// wave-synchronous LDS hand-over between lanes of one wave
+__device__ __forceinline__ void sp_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ void sp_jlist_flush(const SpParams &P, unsigned part, const unsigned *buf, unsigned cnt,
+                                               unsigned lane)
+{
+    sp_wave_sync();
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(&P.ctl[SP_JLIST + part * SP_JSTRIDE], (unsigned long long)cnt);
+    b = __shfl(b, 0);
+    unsigned *list = P.jlist + (size_t)part * P.jcap;
+    for (unsigned t = lane; t < cnt; t += 64) {
+        const unsigned c32 = buf[t];
+        if (b + t < P.jcap) list[b + t] = c32;
+        else atomicOr(&P.ctl[SP_ERR], 4ull);   // cannot happen: a part holds every cell its blocks visit
+    }
+    sp_wave_sync();
+}
+
 __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 {
+    __shared__ unsigned s_list[4][SP_JWAVE];
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so XCD x walks the x-th
     // contiguous eighth of the grid -- the neighbour planes a cell reads sit in its own L2.
     const bool xcd = gridDim.x % 8 == 0;
     const unsigned long long span = xcd ? (P.n + 7) / 8 : P.n;
     const unsigned long long base = xcd ? (unsigned long long)(blockIdx.x % 8) * span : 0ull;
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD
+    unsigned *buf = s_list[threadIdx.x >> 6];
+    unsigned cnt = 0;   // wave-uniform
     const unsigned long long first = (unsigned long long)(xcd ? blockIdx.x / 8 : blockIdx.x) * blockDim.x + threadIdx.x;
     const unsigned long long step = (unsigned long long)(xcd ? gridDim.x / 8 : gridDim.x) * blockDim.x;
-    for (unsigned long long it = first; it < span; it += step) {
+    for (unsigned long long it = first; it - lane < span; it += step) {   // wave-uniform trip count
         const unsigned long long c = base + it;
-        if (c >= P.n) break;
+        const bool valid = it < span && c < P.n;
         const unsigned c32 = (unsigned)c;   // n < 2^32 (sparse_sweep_supported)
         const int i = (int)(c32 % (unsigned)P.ni);
         const unsigned r = c32 / (unsigned)P.ni;
         const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
-        const unsigned long long s = P.S[c];
-        if (!sp_in(P, i, j, k)) {
-            P.X[c] = s;
-            continue;
+        unsigned f = 0;
+        if (valid) {
+            const unsigned long long s = P.S[c];
+            int lab[7];
+            if (sp_in(P, i, j, k)) f = sp_mask<false>(P, P.S, i, j, k, c, s, lab);
+            if (!f) P.X[c] = s;
         }
-        const unsigned long long y = sp_eval<false>(P, P.S, i, j, k, c, s);
-        P.X[c] = y;
-        if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) sp_request_downstream(P, i, j, k, c, false);
+        const unsigned long long want = __ballot(f != 0u);
+        if (f) buf[cnt + __builtin_popcountll(want & ((1ull << lane) - 1ull))] = c32;
+        cnt += (unsigned)__builtin_popcountll(want);
+        if (cnt > SP_JWAVE - 64) {
+            sp_jlist_flush(P, part, buf, cnt, lane);
+            cnt = 0;
+        }
     }
+    if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
+}
+
+// Pass 1b: the listed cells, each exactly as in place (sp_eval against S).
+__global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
+{
+    const unsigned part = blockIdx.x % SP_JPARTS;
+    const unsigned long long cnt0 = P.ctl[SP_JLIST + part * SP_JSTRIDE];
+    const unsigned long long cnt = cnt0 < P.jcap ? cnt0 : P.jcap;
+    const unsigned *list = P.jlist + (size_t)part * P.jcap;
+    for (unsigned long long x = (unsigned long long)(blockIdx.x / SP_JPARTS) * blockDim.x + threadIdx.x; x < cnt;
+         x += (unsigned long long)(gridDim.x / SP_JPARTS) * blockDim.x)
+        sp_jacobi_cell(P, list[x]);
 }
 
 // Pass 2: drain the recheck work list.  One lane = one worker; chains are followed
@@ -330,9 +429,9 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 struct SparseSweepWorkspace {
     int workers = SP_WORKERS_DEFAULT;            // repair-kernel workgroups (diagnostics may lower it)
     unsigned long long *alt = nullptr;   // the second state buffer
-    unsigned *req = nullptr, *queue = nullptr;
+    unsigned *req = nullptr, *queue = nullptr, *jlist = nullptr;
     unsigned long long *ctl = nullptr;
-    size_t cap_alt = 0, cap_req = 0, cap_queue = 0;
+    size_t cap_alt = 0, cap_req = 0, cap_queue = 0, cap_jlist = 0;
 };
 
 inline bool sparse_sweep_supported(unsigned long long n, int ni, int nj, int nk)
@@ -371,13 +470,25 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         if (hipMemset(W.ctl, 0, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -4;
     }
     // per sweep: reset the list counters; error bits and statistics accumulate over the call
-    if (hipMemsetAsync(W.ctl, 0, 3 * sizeof(unsigned long long), st) != hipSuccess) return -4;
+    if (hipMemsetAsync(W.ctl + SP_QUEUE, 0, (SP_NCTL - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
+        return -4;
+    unsigned long long blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    blocks = (blocks + 7) / 8 * 8;   // a multiple of the 8 XCDs (k_sp_jacobi's traversal)
+    // each list part holds every cell its blocks visit (~n/64), so it never overflows; sizing
+    // it for the ~10 % that are listed would need an in-place fallback whose registers
+    // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it
+    const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
+    const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
+    if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false)) return -5;
     SpParams P;
     P.soup = soup;
     P.S = *cell;
     P.X = W.alt;
     P.req = W.req;
     P.queue = W.queue;
+    P.jlist = W.jlist;
+    P.jcap = jcap;
     P.ctl = W.ctl;
     P.cap = cap;
     P.n = n;
@@ -403,10 +514,10 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
             }
         }
     }
-    unsigned long long blocks = (n + 255) / 256;
-    if (blocks > 16384) blocks = 16384;
-    blocks = (blocks + 7) / 8 * 8;   // a multiple of the 8 XCDs (k_sp_jacobi's traversal)
     hipLaunchKernelGGL(k_sp_jacobi, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    if (hipGetLastError() != hipSuccess) return -4;
+    const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
+    hipLaunchKernelGGL(k_sp_jlist, dim3((unsigned)lblocks), dim3(256), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
     hipLaunchKernelGGL(k_sp_recheck, dim3(nw), dim3(64), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
@@ -425,6 +536,7 @@ inline void sparse_sweep_release(SparseSweepWorkspace &W)
     (void)hipFree(W.alt);
     (void)hipFree(W.req);
     (void)hipFree(W.queue);
+    (void)hipFree(W.jlist);
     (void)hipFree(W.ctl);
     W = SparseSweepWorkspace();
 }
