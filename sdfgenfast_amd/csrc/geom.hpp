@@ -141,11 +141,20 @@ SDF_HD float ptd_nb(f3 x0, f3 x1, f3 x2, f3 x3)
 // branches).  Every lane still performs exactly ptd_nb's operations for the case it takes,
 // so the result is bit-identical; away from the surface (points project outside the tiny
 // triangles) whole waves skip the inside block.
-__device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3)
+// The triangle-only reciprocal of ptd's barycentric solve, exactly as ptd computes it.  The
+// device kernels take it precomputed (k_prep_soup stores it in the third vertex's w), which
+// takes a division off every distance's dependency chain.
+SDF_HD float tri_invdet(f3 x1, f3 x2, f3 x3)
+{
+    const f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3);
+    const float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
+    return div_rn(1.0f, fmax_std(m13 * m23 - d * d, 1e-30f));
+}
+
+__device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3, float invdet)
 {
     f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3), x03 = sub3(x0, x3);
     float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
-    float invdet = div_rn(1.0f, fmax_std(m13 * m23 - d * d, 1e-30f));
     float a = dot3(x13, x03), b = dot3(x23, x03);
     float w23 = invdet * (m23 * a - d * b);
     float w31 = invdet * (m13 * b - d * a);
@@ -205,14 +214,13 @@ __device__ __forceinline__ f2v psd2(f3x2 x0, f3x2 x1, f3x2 x2)
     const f3x2 p = f3x2{x1.x * s12 + x2.x * w, x1.y * s12 + x2.y * w, x1.z * s12 + x2.z * w};
     return dist3x2(x0, p);
 }
-__device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, f3 x0b, f3 x1b, f3 x2b, f3 x3b, float &da,
-                                          float &db)
+__device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, float inva, f3 x0b, f3 x1b, f3 x2b, f3 x3b,
+                                          float invb, float &da, float &db)
 {
     const f3x2 x0 = mk3x2(x0a, x0b), x1 = mk3x2(x1a, x1b), x2 = mk3x2(x2a, x2b), x3 = mk3x2(x3a, x3b);
     const f3x2 x13 = sub3x2(x1, x3), x23 = sub3x2(x2, x3), x03 = sub3x2(x0, x3);
     const f2v m13 = mag2x2(x13), m23 = mag2x2(x23), d = dot3x2(x13, x23);
-    const f2v det = m13 * m23 - d * d;
-    const f2v invdet = f2v{div_rn(1.0f, fmax_std(det.x, 1e-30f)), div_rn(1.0f, fmax_std(det.y, 1e-30f))};
+    const f2v invdet = f2v{inva, invb};   // tri_invdet of each triangle
     const f2v a = dot3x2(x13, x03), b = dot3x2(x23, x03);
     const f2v w23 = invdet * (m23 * a - d * b);
     const f2v w31 = invdet * (m13 * b - d * a);

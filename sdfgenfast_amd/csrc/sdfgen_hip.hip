@@ -75,6 +75,7 @@ __global__ void k_prep_soup(const uint32_t *__restrict__ tri, uint64_t ntri, con
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < ntri;
          t += (uint64_t)gridDim.x * blockDim.x) {
         uint32_t v[3] = {tri[3 * t + 0], tri[3 * t + 1], tri[3 * t + 2]};
+        f3 x[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             uint64_t q = v[c];
@@ -82,8 +83,12 @@ __global__ void k_prep_soup(const uint32_t *__restrict__ tri, uint64_t ntri, con
                 atomicOr(err_flag, 1);
                 q = 0;
             }
-            soup[3 * t + c] = make_float4(xyz[3 * q + 0], xyz[3 * q + 1], xyz[3 * q + 2], 0.0f);
+            x[c] = mk3(xyz[3 * q + 0], xyz[3 * q + 1], xyz[3 * q + 2]);
         }
+        // w of the third vertex: the triangle's tri_invdet (read by every ptd_wave / ptd_wave2)
+        soup[3 * t + 0] = make_float4(x[0].x, x[0].y, x[0].z, 0.0f);
+        soup[3 * t + 1] = make_float4(x[1].x, x[1].y, x[1].z, 0.0f);
+        soup[3 * t + 2] = make_float4(x[2].x, x[2].y, x[2].z, tri_invdet(x[0], x[1], x[2]));
     }
 }
 
@@ -252,10 +257,10 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
             const f3 gx2 = mk3((float)i2 * g.dx + g.ox, (float)j2 * g.dx + g.oy, (float)k2 * g.dx + g.oz);
             float d, d2 = 0.0f;
             if (__any(two)) {
-                ptd_wave2(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2), gx2,
-                          load_vtx(soup, t2, 0), load_vtx(soup, t2, 1), load_vtx(soup, t2, 2), d, d2);
+                ptd_wave2(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2), soup[3 * t + 2].w, gx2,
+                          load_vtx(soup, t2, 0), load_vtx(soup, t2, 1), load_vtx(soup, t2, 2), soup[3 * t2 + 2].w, d, d2);
             } else {
-                d = ptd_wave(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2));
+                d = ptd_wave(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2), soup[3 * t + 2].w);
             }
             emit(d, i, j, k, t);
             if (two) emit(d2, i2, j2, k2, t2);
@@ -376,7 +381,8 @@ __global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__
         const uint64_t q2 = (q ^ 1) < n ? (q ^ 1) : q;
         const float *r = pts + 12 * q2;
         float da, db;
-        ptd_wave2(x0, x1, x2, x3, x0, mk3(r[3], r[4], r[5]), mk3(r[6], r[7], r[8]), mk3(r[9], r[10], r[11]), da, db);
+        const f3 y1 = mk3(r[3], r[4], r[5]), y2 = mk3(r[6], r[7], r[8]), y3 = mk3(r[9], r[10], r[11]);
+        ptd_wave2(x0, x1, x2, x3, tri_invdet(x1, x2, x3), x0, y1, y2, y3, tri_invdet(y1, y2, y3), da, db);
         out[q] = da;
         (void)db;
         return;
@@ -385,13 +391,14 @@ __global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__
         const uint64_t q2 = (q ^ 1) < n ? (q ^ 1) : q;
         const float *r = pts + 12 * q2;
         float da, db;
-        ptd_wave2(mk3(r[0], r[1], r[2]), mk3(r[3], r[4], r[5]), mk3(r[6], r[7], r[8]), mk3(r[9], r[10], r[11]), x0,
-                  x1, x2, x3, da, db);
+        const f3 y1 = mk3(r[3], r[4], r[5]), y2 = mk3(r[6], r[7], r[8]), y3 = mk3(r[9], r[10], r[11]);
+        ptd_wave2(mk3(r[0], r[1], r[2]), y1, y2, y3, tri_invdet(y1, y2, y3), x0, x1, x2, x3, tri_invdet(x1, x2, x3),
+                  da, db);
         out[q] = db;
         (void)da;
         return;
     }
-    out[q] = variant == 0 ? ptd(x0, x1, x2, x3) : (variant == 1 ? ptd_nb(x0, x1, x2, x3) : ptd_wave(x0, x1, x2, x3));
+    out[q] = variant == 0 ? ptd(x0, x1, x2, x3) : (variant == 1 ? ptd_nb(x0, x1, x2, x3) : ptd_wave(x0, x1, x2, x3, tri_invdet(x1, x2, x3)));
 }
 
 __global__ void k_debug_pit2d(uint64_t n, const double *__restrict__ in, double *__restrict__ out)

@@ -185,8 +185,8 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
         const float4 a0 = P.soup[ba], a1 = P.soup[ba + 1], a2 = P.soup[ba + 2];
         const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
         float da, db;
-        ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), gx,
-                  mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), da, db);
+        ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w, gx,
+                  mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), b2.w, da, db);
         if (has_a && da < phi) {
             phi = da;
             ct = ta;

@@ -470,8 +470,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                                 e1 = ent[q];
                                 t1 = lab[q];
                             }
+                        const float4 v3 = s_ent[3 * e1 + 2];
                         const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]),
-                                               st_xyz(s_ent[3 * e1 + 2]));
+                                               st_xyz(v3), v3.w);
                         if (d < phi) {
                             phi = d;
                             ct = t1;
@@ -506,13 +507,15 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
                                             c0 + ST_CLW * w + (l2 >> 3));
                         float d1, d2;
-                        ptd_wave2(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]), g2,
-                                  st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(s_ent[3 * e2 + 2]), d1, d2);
+                        const float4 v13 = s_ent[3 * e1 + 2], v23 = s_ent[3 * e2 + 2];
+                        ptd_wave2(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(v13), v13.w, g2,
+                                  st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(v23), v23.w, d1, d2);
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
                         if (has2) s_d[w][((p2 >> 6) & 7) * ST_CPW + l2] = d2;
                     } else {
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] =
-                            ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]));
+                            ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]),
+                                     s_ent[3 * e1 + 2].w);
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
