@@ -30,6 +30,7 @@ import argparse
 import hashlib
 import json
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -210,14 +211,22 @@ def zslab_child(world, workload, timeout=600):
            "--gpus", str(world), "--mode", "zslab", "--workload", workload, "--steps", "2", "--warmup", "1",
            "--no-zslab", "--no-cpu-baseline"]
     t0 = time.time()
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=ROOT,
+                         start_new_session=True)
     try:
-        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT,
-                           start_new_session=True)
+        out, err = p.communicate(timeout=timeout)
     except subprocess.TimeoutExpired:
+        # the launcher and its ranks share the new session's process group: end all of them,
+        # so no orphaned rank keeps a GPU busy under the measurement that follows
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+        p.communicate()
         return {"workload": workload, "n_gpus": world, "error": f"timed out after {timeout} s"}
-    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    lines = [x for x in out.splitlines() if x.startswith("{")]
     if p.returncode != 0 or not lines:
-        tail = (p.stderr or "").strip().splitlines()[-3:]
+        tail = (err or "").strip().splitlines()[-3:]
         return {"workload": workload, "n_gpus": world, "error": f"rc={p.returncode}: {' | '.join(tail)[-400:]}"}
     res = json.loads(lines[-1])
     return {"workload": workload, "n_gpus": world, "parallelism": res["config"]["parallelism"],
