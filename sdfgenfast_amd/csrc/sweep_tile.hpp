@@ -233,7 +233,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
     __shared__ float s_d[ST_NCW][7 * ST_CPW];      // per compute wave: distance of candidate q for lane
     // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
-    // compute wave w -- one 16-byte word, so a readiness poll is one ds_read_b128.
+    // compute wave w.
     __shared__ __attribute__((aligned(16))) int s_hdr[4];
     // halo entries < s_halo_ready[s] are in LDS; the extra last word is never "not ready"
     // (the stream index of lanes that read no halo stream)
@@ -392,9 +392,12 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
                 unsigned long long tw0 = 0;
                 for (;;) {
-                    // branch-free: one 16-byte header read + the (up to 3) halo streams this
-                    // lane reads at this step (the dummy word for lanes off the tile edge)
-                    const i4v H = *reinterpret_cast<volatile i4v *>(s_hdr);
+                    // branch-free: the 4 header words + the (up to 3) halo streams this lane
+                    // reads at this step (the dummy word for lanes off the tile edge), 7 ds_read_b32
+                    // issued together.  (A volatile 16-byte read of s_hdr through a generic pointer
+                    // compiled to a FLAT load: vector-memory latency on every poll, 8 % of the
+                    // first pass at 256^3, 14 % at 512^3.)
+                    const i4v H = i4v{lds_ld(&s_hdr[0]), lds_ld(&s_hdr[1]), lds_ld(&s_hdr[2]), lds_ld(&s_hdr[3])};
                     const int rA = lds_ld(&s_halo_ready[hsA]), rB = lds_ld(&s_halo_ready[hsB]),
                               rC = lds_ld(&s_halo_ready[hsC]);
                     const bool own_ok = H.x > h;
