@@ -43,6 +43,7 @@ import numpy as np  # noqa: E402
 
 METRIC = "Mvoxels/sec at 256³ (1M-tri mesh); achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_ISSUE_PEAK = 256 * 4 * 2.4e9 / 2   # wave64 VALU instructions/s: 256 CUs x 4 SIMDs, 2 cycles each
 SWEEP_BYTES_PER_CELL = 16   # read phi+ct (8 B) + write phi+ct (8 B) per cell per sweep
 PARITY_OK = "bit-exact vs reference (sha256 of phi)"
 
@@ -296,6 +297,21 @@ def main():
             k = rec.get("kernels", {}).get("k_sweep_tile")
             if rec.get("workload") == args.workload and k:
                 traffic, traffic_src = k["hbm_bytes_per_launch"], "profiles/pmc_summary.json"
+        # SURVEY 8.d caveat: the sweep is latency/VALU-bound, so also report its VALU issue rate
+        # (SQ_INSTS_VALU per launch from profiles/pmc_sq_summary.json, tools/pmc_sq.sh) against
+        # the chip's: one wave64 VALU instruction per 2 cycles per SIMD (MI355X_MICROARCH.md)
+        valu = None
+        sp = os.path.join(ROOT, "profiles", "pmc_sq_summary.json")
+        if os.path.exists(sp) and mode != "zslab" and r["launch_ms"] > 0:
+            rec = json.load(open(sp))
+            k = next((v for n, v in rec.get("kernels", {}).items() if n.startswith("k_sweep_tile")), None)
+            if rec.get("workload") == args.workload and k and "SQ_INSTS_VALU" in k:
+                peak = VALU_ISSUE_PEAK
+                rate = k["SQ_INSTS_VALU"] / (r["launch_ms"] * 1e-3)
+                valu = {"kernel": "k_sweep_tile", "insts_per_launch": int(k["SQ_INSTS_VALU"]),
+                        "achieved": round(rate / 1e9, 2), "peak": round(peak / 1e9, 1),
+                        "unit": "G wave-instructions/s", "frac": round(rate / peak, 4),
+                        "source": "profiles/pmc_sq_summary.json"}
         res = {
             "metric": METRIC,
             "value": round(r["value"], 3),
@@ -320,6 +336,7 @@ def main():
                          "sweeps_per_launch": r["sweeps_per_launch"],
                          "launches_per_step": r["n_tile"], "avg_launch_ms": round(r["launch_ms"], 5),
                          "algorithmic_bytes_per_launch": int(r["bytes_per_launch"])},
+            "valu": valu,
             "phases_ms": r["phases"],
             "sweep_impl": r["sweep_impl"],
             "parity": r["parity"],

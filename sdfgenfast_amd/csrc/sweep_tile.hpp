@@ -461,6 +461,13 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         fmask |= (skip ? 0u : 1u) << q;
                     }
                 }
+#ifdef ST_VALU_PROBE   // diagnostics: a dependent chain of N extra VALU per compute step
+                {
+                    int x_ = L;
+#pragma unroll
+                    for (int i_ = 0; i_ < ST_VALU_PROBE; ++i_) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x_));
+                }
+#endif
                 // ---- at most one candidate per cell (the common case away from the surface):
                 //      each cell lane evaluates its own, no compaction and no LDS exchange ----
                 const bool single = __all(__popc(fmask) <= 1);

@@ -17,7 +17,13 @@ for f in glob.glob("gpurun_out/pmc_sq/**/*counter_collection.csv", recursive=Tru
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"].split("(")[0].split("::")[-1][:40]
         per[n][r["Counter_Name"]] += float(r["Counter_Value"]); disp[n].add(r["Dispatch_Id"])
+import json, os
+out = {"workload": sys.argv[1], "units": "per launch (summed over the chip's counter instances)", "kernels": {}}
 for n, c in per.items():
     d = len(disp[n])
     print(f"{n:42s} launches {d:3d} " + " ".join(f"{k}={v/d:.4g}" for k, v in sorted(c.items())))
+    if n.strip():
+        out["kernels"][n.strip()] = {"launches": d, **{k: v / d for k, v in sorted(c.items())}}
+os.makedirs("profiles", exist_ok=True)
+json.dump(out, open("profiles/pmc_sq_summary.json", "w"), indent=1)
 PY
