@@ -65,6 +65,9 @@ namespace sdfhip {
 #ifndef ST_G_DEF
 #define ST_G_DEF 2     // helper batch: steps / halo entries per global round trip (2 or 4)
 #endif
+#ifndef ST_WORK_PRIO
+#define ST_WORK_PRIO 2   // compute waves' issue priority while stepping (0 while they wait)
+#endif
 #ifndef ST_WPE_DEF
 #define ST_WPE_DEF 3   // waves per SIMD the register budget must allow
 #endif
@@ -359,7 +362,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             const int col_id = cl * ST_T + bl;
             const int b = b0 + bl, c = c0 + cl;
             const bool col = cell_lane && b < P.B && c < P.ce;
-            __builtin_amdgcn_s_setprio(2);
+            __builtin_amdgcn_s_setprio(ST_WORK_PRIO);
             int nb_base[7], nb_stride[7], nb_mask[7];
             {
                 auto ring = [&](int q, int lbl, int lcl) {
@@ -412,6 +415,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                     ++n_cpoll;
                     if (!__all(own_ok)) ++n_cpoll_own;
+                    // a waiting wave yields its SIMD's issue slots to the working waves there (the
+                    // step is issue-latency bound: -3 % first pass at 256^3)
+                    __builtin_amdgcn_s_setprio(0);
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
                         if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
                         h = nsteps;
@@ -422,6 +428,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     else if (polls < 64) __builtin_amdgcn_s_sleep(2);
                     else __builtin_amdgcn_s_sleep(8);
                 }
+                __builtin_amdgcn_s_setprio(ST_WORK_PRIO);
                 asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
                 if (TRACE && tw0) t_wait += wall_clock64() - tw0;
                 if (h >= nsteps) break;
@@ -461,6 +468,14 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         fmask |= (skip ? 0u : 1u) << q;
                     }
                 }
+#ifdef ST_LDS_PROBE   // diagnostics: a dependent chain of N extra LDS reads per compute step
+                {
+                    int x_ = 0;
+#pragma unroll
+                    for (int i_ = 0; i_ < ST_LDS_PROBE; ++i_) x_ = lds_ld(&s_abort + (x_ & 0x40000000));
+                    asm volatile("" ::"v"(x_));
+                }
+#endif
 #ifdef ST_VALU_PROBE   // diagnostics: a dependent chain of N extra VALU per compute step
                 {
                     int x_ = L;
