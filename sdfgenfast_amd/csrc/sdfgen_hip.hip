@@ -193,24 +193,33 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
                     }
             }
         }
-        __syncthreads();
-        if (tid == 0) {
-            unsigned acc = 0;
-            int ui0 = INT_MAX, uj0 = INT_MAX, uk0 = INT_MAX, ui1 = -1, uj1 = -1, uk1 = -1;
-            for (int q = 0; q < nb; ++q) {
-                const BandBox B = s_box[q];
-                s_pre[q] = acc;
-                acc += (unsigned)(B.bi * B.bj * B.bk);
-                if (B.bi) {
-                    ui0 = min(ui0, B.i0); uj0 = min(uj0, B.j0); uk0 = min(uk0, B.k0);
-                    ui1 = max(ui1, B.i0 + B.bi - 1); uj1 = max(uj1, B.j0 + B.bj - 1); uk1 = max(uk1, B.k0 + B.bk - 1);
-                }
+        if (tid < 64) {
+            // wave 0: prefix sums of the box volumes and the union box across lanes (lane q =
+            // triangle q; lanes >= nb carry empty boxes) -- no single-thread loop
+            BandBox B{0, 0, 0, 0, 0, 0};
+            if (tid < nb) B = s_box[tid];
+            const unsigned vol = (unsigned)(B.bi * B.bj * B.bk);
+            unsigned incl = vol;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const unsigned y = __shfl_up(incl, d);
+                if (tid >= d) incl += y;
             }
-            s_pre[nb] = acc;
-            s_u[0] = ui0; s_u[1] = uj0; s_u[2] = uk0;
-            s_u[3] = ui1 >= ui0 ? ui1 - ui0 + 1 : 0;
-            s_u[4] = uj1 >= uj0 ? uj1 - uj0 + 1 : 0;
-            s_u[5] = uk1 >= uk0 ? uk1 - uk0 + 1 : 0;
+            if (tid < nb) s_pre[tid] = incl - vol;
+            if (tid == nb - 1) s_pre[nb] = incl;
+            int ui0 = B.bi ? B.i0 : INT_MAX, uj0 = B.bi ? B.j0 : INT_MAX, uk0 = B.bi ? B.k0 : INT_MAX;
+            int ui1 = B.bi ? B.i0 + B.bi - 1 : -1, uj1 = B.bi ? B.j0 + B.bj - 1 : -1, uk1 = B.bi ? B.k0 + B.bk - 1 : -1;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) {
+                ui0 = min(ui0, __shfl_xor(ui0, d)); uj0 = min(uj0, __shfl_xor(uj0, d)); uk0 = min(uk0, __shfl_xor(uk0, d));
+                ui1 = max(ui1, __shfl_xor(ui1, d)); uj1 = max(uj1, __shfl_xor(uj1, d)); uk1 = max(uk1, __shfl_xor(uk1, d));
+            }
+            if (tid == 0) {
+                s_u[0] = ui0; s_u[1] = uj0; s_u[2] = uk0;
+                s_u[3] = ui1 >= ui0 ? ui1 - ui0 + 1 : 0;
+                s_u[4] = uj1 >= uj0 ? uj1 - uj0 + 1 : 0;
+                s_u[5] = uk1 >= uk0 ? uk1 - uk0 + 1 : 0;
+            }
         }
         __syncthreads();
         const unsigned total = s_pre[nb];
