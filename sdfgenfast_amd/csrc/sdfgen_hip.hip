@@ -124,8 +124,15 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 // A batch whose union box does not fit the LDS table falls back to direct global
 // atomics.  min() is order-independent, so the result is the one-triangle-at-a-time
 // result bit for bit.
-constexpr int BAND_BT = 32;             // triangles per batch
-constexpr int BAND_LDS = 5120;          // u64 keys in the LDS table (40 KB)
+#ifndef BAND_BT_DEF
+#define BAND_BT_DEF 32
+#endif
+#ifndef BAND_LDS_DEF
+#define BAND_LDS_DEF 5120
+#endif
+constexpr int BAND_BT = BAND_BT_DEF;    // triangles per batch (<= 64: one wave sets a batch up)
+constexpr int BAND_LDS = BAND_LDS_DEF;  // u64 keys in the LDS table (40 KB)
+static_assert(BAND_BT >= 1 && BAND_BT <= 64, "a batch's boxes are scanned by one wave");
 
 struct BandBox {
     int i0, j0, k0, bi, bj, bk;         // clamped band box (bi*bj*bk cells; 0 = empty)
