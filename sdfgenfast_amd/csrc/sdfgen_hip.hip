@@ -452,6 +452,8 @@ struct Workspace {
     std::mutex mu;
     TileSweepWorkspace wf;
     SparseSweepWorkspace sp;
+    float *out = nullptr;               // phi of the host-buffer entry point before its copy-out
+    size_t cap_out = 0;
 };
 
 std::mutex g_mu;
@@ -1036,8 +1038,8 @@ int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
     const uint64_t n = (uint64_t)ni * nj * nk;
     if ((rc = grow(&ws->tri, &ws->cap_tri, std::max<uint64_t>(3 * ntri, 1), err))) return rc;
     if ((rc = grow(&ws->xyz, &ws->cap_xyz, std::max<uint64_t>(3 * nvert, 1), err))) return rc;
-    float *d_out = nullptr;
-    HIPCHK(hipMalloc((void **)&d_out, n * sizeof(float)));
+    if ((rc = grow(&ws->out, &ws->cap_out, n, err))) return rc;
+    float *d_out = ws->out;
     hipStream_t st = ws->stream;
     if (ntri) {
         HIPCHK(hipMemcpyAsync(ws->tri, tri, 3 * ntri * sizeof(uint32_t), hipMemcpyHostToDevice, st));
@@ -1046,11 +1048,12 @@ int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
     rc = run_pipeline(ws, st, ws->tri, ntri, ws->xyz, nvert, origin, dx, ni, nj, nk, exact_band, out_layout, d_out,
                       err);
     if (rc == 0) {
+        // a pageable copy: its cost here is mostly first-touch page faults of the caller's
+        // fresh buffer (a pinned, 8-thread staged copy-out measured no faster)
         hipError_t e = hipMemcpyAsync(phi_out, d_out, n * sizeof(float), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) rc = err.set(SDFGEN_HIP_ERUNTIME, "GPU (HIP) error %s copying phi", hipGetErrorName(e));
     }
-    hipFree(d_out);
     return rc;
 }
 
@@ -1097,6 +1100,7 @@ int sdfgen_hip_release(void)
         hipFree(w->xyz);
         hipFree(w->err_flag);
         hipFree(w->evals);
+        hipFree(w->out);
         tile_sweep_release(w->wf);
         sparse_sweep_release(w->sp);
         for (auto &e : w->ev) hipEventDestroy(e);
