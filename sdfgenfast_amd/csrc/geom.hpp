@@ -84,6 +84,21 @@ SDF_HD float psd(f3 x0, f3 x1, f3 x2)
     return dist3(x0, p);
 }
 
+// psd before its final sqrt: the squared distance (the device kernels take ONE correctly
+// rounded sqrt of the smallest candidate, see ptd_wave)
+SDF_HD float psd_sq(f3 x0, f3 x1, f3 x2)
+{
+    f3 e = sub3(x2, x1);
+    double m2 = (double)mag2(e);
+    f3 t = sub3(x2, x0);
+    float s12 = (float)((double)dot3(t, e) / m2);
+    if (s12 < 0.0f) s12 = 0.0f;
+    else if (s12 > 1.0f) s12 = 1.0f;
+    float w = 1.0f - s12;
+    f3 d = sub3(x0, mk3(x1.x * s12 + x2.x * w, x1.y * s12 + x2.y * w, x1.z * s12 + x2.z * w));
+    return (d.x * d.x + d.y * d.y) + d.z * d.z;
+}
+
 // point_triangle_distance.
 SDF_HD float ptd(f3 x0, f3 x1, f3 x2, f3 x3)
 {
@@ -160,21 +175,25 @@ __device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3, float invd
     float w31 = invdet * (m13 * b - d * a);
     float w12 = (1.0f - w23) - w31;
     const bool inside = (w23 >= 0.0f) & (w31 >= 0.0f) & (w12 >= 0.0f);
-    float r = 0.0f;
+    // One sqrt for all branches: the reference returns sqrt(inside) or min(sqrt(e1), sqrt(e2));
+    // a correctly rounded sqrt is monotone, so min(sqrt(e1), sqrt(e2)) == sqrt(min(e1, e2)) bit
+    // for bit (with std::min's argument order, NaN included; squared sums are never -0).
+    float r2 = 0.0f;
     if (__any(inside)) {
         f3 p = mk3((x1.x * w23 + x2.x * w31) + x3.x * w12,
                    (x1.y * w23 + x2.y * w31) + x3.y * w12,
                    (x1.z * w23 + x2.z * w31) + x3.z * w12);
-        r = dist3(x0, p);
+        const f3 dd = sub3(x0, p);
+        r2 = (dd.x * dd.x + dd.y * dd.y) + dd.z * dd.z;
     }
     if (__any(!inside)) {
         const bool c23 = w23 > 0.0f, c31 = !c23 & (w31 > 0.0f);
         const f3 fb = (c23 | c31) ? x2 : x3;
         const f3 sa = c23 ? x1 : x2;
-        const float d_edge = fmin_std(psd(x0, x1, fb), psd(x0, sa, x3));
-        r = inside ? r : d_edge;
+        const float e2 = fmin_std(psd_sq(x0, x1, fb), psd_sq(x0, sa, x3));
+        r2 = inside ? r2 : e2;
     }
-    return r;
+    return sqrt_rn(r2);
 }
 
 // Two point-triangle distances per lane in packed FP32 (v_pk_mul_f32 / v_pk_add_f32: each
@@ -212,7 +231,8 @@ __device__ __forceinline__ f2v psd2(f3x2 x0, f3x2 x1, f3x2 x2)
     s12.y = (s12.y < 0.0f) ? 0.0f : ((s12.y > 1.0f) ? 1.0f : s12.y);
     const f2v w = 1.0f - s12;
     const f3x2 p = f3x2{x1.x * s12 + x2.x * w, x1.y * s12 + x2.y * w, x1.z * s12 + x2.z * w};
-    return dist3x2(x0, p);
+    const f3x2 d = sub3x2(x0, p);
+    return (d.x * d.x + d.y * d.y) + d.z * d.z;   // squared (see ptd_wave: one sqrt at the end)
 }
 __device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, float inva, f3 x0b, f3 x1b, f3 x2b, f3 x3b,
                                           float invb, float &da, float &db)
@@ -227,11 +247,12 @@ __device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, float 
     const f2v w12 = (1.0f - w23) - w31;
     const bool ia = (w23.x >= 0.0f) & (w31.x >= 0.0f) & (w12.x >= 0.0f);
     const bool ib = (w23.y >= 0.0f) & (w31.y >= 0.0f) & (w12.y >= 0.0f);
-    f2v r = f2v{0.0f, 0.0f};
+    f2v r = f2v{0.0f, 0.0f};   // squared distances until the end (see ptd_wave)
     if (__any(ia | ib)) {
         const f3x2 p = f3x2{(x1.x * w23 + x2.x * w31) + x3.x * w12, (x1.y * w23 + x2.y * w31) + x3.y * w12,
                             (x1.z * w23 + x2.z * w31) + x3.z * w12};
-        r = dist3x2(x0, p);
+        const f3x2 dd = sub3x2(x0, p);
+        r = (dd.x * dd.x + dd.y * dd.y) + dd.z * dd.z;
     }
     if (__any(!ia | !ib)) {
         const bool c23a = w23.x > 0.0f, c31a = !c23a & (w31.x > 0.0f);
@@ -242,8 +263,8 @@ __device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, float 
         const f2v de = f2v{fmin_std(first.x, second.x), fmin_std(first.y, second.y)};
         r = sel2(ia, ib, r, de);
     }
-    da = r.x;
-    db = r.y;
+    da = sqrt_rn(r.x);
+    db = sqrt_rn(r.y);
 }
 
 // orientation (SOS-robust 2D), FP64.
