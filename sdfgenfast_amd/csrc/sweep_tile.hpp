@@ -545,17 +545,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
                 // ---- apply in the reference check order: strict '<', first minimum wins ----
-                if (act) {
+                if (act) {   // branch-free: all 7 slots read at once, non-candidates masked out
+                    float dq[7];
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) dq[q] = s_d[w][q * ST_CPW + L];
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
-                        if ((fmask >> q) & 1u) {
-                            const float d = s_d[w][q * ST_CPW + L];
-                            if (d < phi) {
-                                phi = d;
-                                ct = lab[q];
-                                win = ent[q];
-                            }
-                        }
+                        const bool take = ((fmask >> q) & 1u) && dq[q] < phi;
+                        phi = take ? dq[q] : phi;
+                        ct = take ? lab[q] : ct;
+                        win = take ? ent[q] : win;
                     }
                 }
                 }
