@@ -233,8 +233,10 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     StParams P = P0;
     constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
-    __shared__ int s_pair[ST_NCW][7 * ST_CPW];     // per compute wave: (entry << 9 | q << 6 | lane) list
-    __shared__ float s_d[ST_NCW][7 * ST_CPW];      // per compute wave: distance of candidate q for lane
+    // per compute wave: (entry << 9 | q << 6 | lane) list, then one trash word per lane (the
+    // target of lanes with nothing to store, so the stores need no divergent branch)
+    __shared__ int s_pair[ST_NCW][7 * ST_CPW + 64];
+    __shared__ float s_d[ST_NCW][7 * ST_CPW + 64];   // per compute wave: distance of candidate q for lane
     // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
     // compute wave w.
     __shared__ __attribute__((aligned(16))) int s_hdr[4];
@@ -512,11 +514,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 for (int q = 0; q < 7; ++q) {
                     const bool f = (fmask >> q) & 1u;
                     const unsigned long long m = __ballot(f);
-                    if (f) {
-                        const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                        s_pair[w][pos] = (ent[q] << 9) | (q << 6) | L;
-                    }
+                    const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    s_pair[w][f ? pos : 7 * ST_CPW + L] = (ent[q] << 9) | (q << 6) | L;
                     total += (int)__popcll(m);
                 }
                 // ---- evaluate (<= 112 pairs): one per lane, a second chain only if needed ----
@@ -536,7 +536,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         ptd_wave2(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(v13), v13.w, g2,
                                   st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(v23), v23.w, d1, d2);
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
-                        if (has2) s_d[w][((p2 >> 6) & 7) * ST_CPW + l2] = d2;
+                        s_d[w][has2 ? ((p2 >> 6) & 7) * ST_CPW + l2 : 7 * ST_CPW + L] = d2;
                     } else {
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] =
                             ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]),
