@@ -125,7 +125,10 @@ __device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned lo
     int lcq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
-        const uint32_t w = (uint32_t)(LIVE ? sp_ld64(L + nb[q]) : L[nb[q]]);
+        // the low word (label, stamp) only: half the bytes of the 8-byte cell (a 32-bit load of
+        // a 64-bit atomically stored word sees one of its stored values' halves)
+        const uint32_t *lw = reinterpret_cast<const uint32_t *>(L + nb[q]);
+        const uint32_t w = LIVE ? sp_ld32(lw) : *lw;
         lab[q] = lbl_of(w);
         lcq[q] = lc_of(w);
     }
