@@ -312,13 +312,23 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
     unsigned cnt = 0;   // wave-uniform
     const unsigned long long first = (unsigned long long)(xcd ? blockIdx.x / 8 : blockIdx.x) * blockDim.x + threadIdx.x;
     const unsigned long long step = (unsigned long long)(xcd ? gridDim.x / 8 : gridDim.x) * blockDim.x;
+    // (i, j, k) of the lane's cell: divided out once, then advanced by the stride's own
+    // (si, sj, sk) with carries (two integer divisions per cell cost ~30 instructions)
+    int i, j, k, si, sj, sk;
+    {
+        const unsigned c0 = (unsigned)(base + first), r0 = c0 / (unsigned)P.ni;
+        i = (int)(c0 % (unsigned)P.ni);
+        j = (int)(r0 % (unsigned)P.nj);
+        k = (int)(r0 / (unsigned)P.nj);
+        const unsigned st = (unsigned)step, rs = st / (unsigned)P.ni;
+        si = (int)(st % (unsigned)P.ni);
+        sj = (int)(rs % (unsigned)P.nj);
+        sk = (int)(rs / (unsigned)P.nj);
+    }
     for (unsigned long long it = first; it - lane < span; it += step) {   // wave-uniform trip count
         const unsigned long long c = base + it;
         const bool valid = it < span && c < P.n;
         const unsigned c32 = (unsigned)c;   // n < 2^32 (sparse_sweep_supported)
-        const int i = (int)(c32 % (unsigned)P.ni);
-        const unsigned r = c32 / (unsigned)P.ni;
-        const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
         unsigned f = 0;
         if (valid) {
             const unsigned long long s = P.S[c];
@@ -333,6 +343,13 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
             sp_jlist_flush(P, part, buf, cnt, lane);
             cnt = 0;
         }
+        i += si;
+        const int ci = i >= P.ni;
+        i -= ci ? P.ni : 0;
+        j += sj + ci;
+        const int cj = j >= P.nj;
+        j -= cj ? P.nj : 0;
+        k += sk + cj;
     }
     if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
 }
