@@ -83,7 +83,7 @@ constexpr int ST_RH = ST_RH_DEF;
 constexpr int ST_G = ST_G_DEF;
 static_assert(ST_NCW >= 1 && ST_NCW <= 3 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
 typedef int i4v __attribute__((ext_vector_type(4)));
-static_assert((ST_RR & (ST_RR - 1)) == 0 && ST_RR >= 4, "ring slots: power of two >= 4");
+static_assert((ST_RR & (ST_RR - 1)) == 0 && ST_RR >= 8, "ring slots: power of two >= 8 (RR = 4 measured wrong results: no lead left between the waves)");
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
 constexpr int ST_LEAD = ST_RR - 4;            // max lead of wave w over wave w+1 (ring hazard)
