@@ -406,8 +406,20 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             const int i = (int)((unsigned)e % (unsigned)P.ni);
             const unsigned r0 = (unsigned)e / (unsigned)P.ni;
             const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
+#ifdef SP_RT_PROBE   // diagnostics: N extra dependent device-scope round trips per evaluation
+            {
+                size_t e2 = e;
+#pragma unroll
+                for (int i_ = 0; i_ < SP_RT_PROBE; ++i_) e2 += (size_t)(sp_ld64(P.X + e2) & 0ull);
+                e = e2;
+            }
+#endif
             const unsigned long long cur = sp_ld64(P.X + e);
+#ifdef SP_NOEVAL_RECHECK   // diagnostics: the work list's own cost (no evaluation, no relabel)
+            const unsigned long long y = cur;
+#else
             const unsigned long long y = sp_eval<true>(P, P.X, i, j, k, e, P.S[e]);
+#endif
             ++runs;
             const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
             if (y != cur) {
