@@ -11,7 +11,11 @@ secs, seed = float(sys.argv[1]), int(sys.argv[2])
 rng = np.random.default_rng(seed)
 t_end = time.time() + secs
 n = bad = cells = 0
+t_note = time.time() + 30
 while time.time() < t_end:
+    if time.time() > t_note:   # progress line: a silent GPU command is taken for hung after 180 s
+        print(f"... {n} cases, {bad} mismatches", flush=True)
+        t_note = time.time() + 30
     if rng.random() < 0.5:
         nv = int(rng.integers(10, 3000))
         v = rng.normal(size=(nv, 3)).astype(np.float32)
