@@ -1,8 +1,11 @@
 // sdfgen/sdfgen_unified.h -- C++ drop-in for the reference's unified API.
 //
-// Same declarations as /root/reference/common/sdfgen_unified.h:16-20, 47-57, 68:
-// a reference caller (python/sdfgen_py.cpp:206-214, app/main.cpp:273,
-// tests/test_utils.cpp:27) compiles unchanged against this header.
+// Same declarations as /root/reference/common/sdfgen_unified.h:16-20, 47-57, 68, over
+// types with the reference's names, template parameters and data layout (vec.h, array1.h,
+// array3.h here): a reference caller (python/sdfgen_py.cpp:206-214, app/main.cpp:273,
+// tests/test_utils.cpp:27) compiled against EITHER this header or the reference's own
+// common/sdfgen_unified.h links to libsdfgen_hip.so unchanged -- the exported symbol is
+// the reference's mangled name (tests/test_cxx_dropin.py builds such callers).
 //   Auto -> GPU when a HIP device is visible, else CPU (common/sdfgen_unified.cpp:42-48)
 //   GPU  -> hand-written gfx950 kernels via include/sdfgen_hip.h; throws
 //           std::runtime_error mentioning "GPU" when no device is usable
@@ -15,6 +18,7 @@
 #include "array3.h"
 #include "vec.h"
 
+#pragma GCC visibility push(default)  // exported from libsdfgen_hip.so (built -fvisibility=hidden)
 namespace sdfgen {
 
 enum class HardwareBackend { Auto, CPU, GPU };
@@ -26,3 +30,4 @@ void make_level_set3(const std::vector<Vec3ui> &tri, const std::vector<Vec3f> &x
 bool is_gpu_available();
 
 }  // namespace sdfgen
+#pragma GCC visibility pop

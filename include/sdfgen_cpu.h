@@ -15,6 +15,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
+#pragma GCC visibility push(default)
 
 enum { SDFGEN_CPU_OK = 0, SDFGEN_CPU_EINVAL = -1, SDFGEN_CPU_EINDEX = -2, SDFGEN_CPU_ENOMEM = -5 };
 
@@ -41,6 +43,7 @@ int sdfgen_cpu_slab_sweep(sdfgen_cpu_slab *s, int sweep, const uint64_t *plane_i
 int sdfgen_cpu_slab_sign(sdfgen_cpu_slab *s, int out_layout, float *phi_slab, char *errbuf, size_t errlen);
 int sdfgen_cpu_slab_destroy(sdfgen_cpu_slab *s);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif

@@ -33,6 +33,8 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
+#pragma GCC visibility push(default)
 
 #define SDFGEN_HIP_ABI_VERSION 1
 
@@ -44,6 +46,10 @@ enum {
     SDFGEN_HIP_ERUNTIME = -4,    /* HIP runtime / kernel error */
     SDFGEN_HIP_ENOMEM = -5       /* device allocation failed */
 };
+
+/* ngpu values of sdfgen_hip_make_level_set3 (any n > 1 is also accepted). */
+#define SDFGEN_NGPU_ALL 0
+#define SDFGEN_NGPU_CURRENT 1
 
 /* Output layouts for phi_out. */
 enum {
@@ -64,12 +70,13 @@ int sdfgen_hip_device_count(void);
  *   xyz      : nvert x 3 float32 positions   (std::vector<Vec3f>::data())
  *   origin   : grid origin (3 floats); dx: cell size; ni,nj,nk: grid dims (> 0)
  *   exact_band: band half-width in cells (cpu_lib/makelevelset3.cpp:210-212)
- *   ngpu     : devices to use.  0 or 1 = the current device.  n > 1 = devices 0..n-1, the
- *              grid split into n Z-slabs driven from this thread (sdfgen_hip_slab_*
- *              sessions connected in-process over peer memory); at most
- *              nk/2 slabs, ENODEV if fewer than n devices are visible.  0 does not mean
- *              "all devices": one grid is bound by the sweeps' dependency chain, so
- *              more GPUs pay off only for large grids.
+ *   ngpu     : devices to use.  SDFGEN_NGPU_ALL (0) = every visible device;
+ *              SDFGEN_NGPU_CURRENT (1) = the current device only (what the reference's GPU
+ *              backend does, gpu_lib/makelevelset3_gpu.cu:600-603, and what the C++ and Python
+ *              drop-ins pass); n > 1 = devices 0..n-1.  With more than one device the grid is
+ *              split into Z-slabs driven from this thread (sdfgen_hip_slab_* sessions connected
+ *              in-process over peer memory), at most nk/2 of them; ENODEV if
+ *              fewer than n devices are visible, EINVAL for n < 0.
  *   out_layout: SDFGEN_LAYOUT_*
  *   phi_out  : caller-allocated ni*nj*nk floats
  */
@@ -180,6 +187,7 @@ int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *ou
  * the SDFGEN_TRACE_SWEEP environment variable in the last call (tasks in dequeue order). */
 int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries, uint64_t *n_out);
 
+#pragma GCC visibility pop
 #ifdef __cplusplus
 }
 #endif

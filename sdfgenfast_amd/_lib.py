@@ -18,6 +18,7 @@ LIB_PATH = os.environ.get("SDFGEN_LIB_OVERRIDE") or os.path.join(_HERE, "libsdfg
 
 OK, EINVAL, EINDEX, ENODEV, ERUNTIME, ENOMEM = 0, -1, -2, -3, -4, -5
 LAYOUT_ARRAY3, LAYOUT_KFAST = 0, 1
+NGPU_ALL, NGPU_CURRENT = 0, 1      # sdfgen_hip_make_level_set3 ngpu (include/sdfgen_hip.h)
 
 _P = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -161,7 +162,7 @@ def device_count() -> int:
 
 
 def make_level_set3(vertices: np.ndarray, triangles: np.ndarray, origin, dx: float, ni: int, nj: int, nk: int,
-                    exact_band: int = 1, layout: int = LAYOUT_KFAST, ngpu: int = 0) -> np.ndarray:
+                    exact_band: int = 1, layout: int = LAYOUT_KFAST, ngpu: int = 1) -> np.ndarray:
     """Host-memory entry (sdfgen_hip_make_level_set3).  Returns phi as a (ni,nj,nk)
     array: C-ordered for LAYOUT_KFAST, a Fortran-ordered view of the i-fastest
     Array3f buffer for LAYOUT_ARRAY3 -- either way phi[i, j, k]."""

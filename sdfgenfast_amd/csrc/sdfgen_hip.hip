@@ -1022,12 +1022,14 @@ int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
     if (rc) return rc;
     if (!phi_out || !origin || (ntri && (!tri || !xyz)))
         return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    if (ngpu < 0) return err.set(SDFGEN_HIP_EINVAL, "ngpu = %d (0 = all devices, 1 = the current device, n > 1)", ngpu);
     const int ndev = device_count_impl();
     if (ndev <= 0) return err.set(SDFGEN_HIP_ENODEV, "GPU backend requested but no HIP GPU device is available");
-    if (ngpu > 1 && nk >= 4) {
-        const int n = std::min(ngpu, nk / 2);
-        if (ngpu > ndev && !getenv("SDFGEN_DEBUG_SLABS_ONE_DEVICE"))
-            return err.set(SDFGEN_HIP_ENODEV, "ngpu = %d but only %d HIP device(s) visible", ngpu, ndev);
+    const int want = ngpu == SDFGEN_NGPU_ALL ? ndev : ngpu;
+    if (want > ndev && !getenv("SDFGEN_DEBUG_SLABS_ONE_DEVICE"))
+        return err.set(SDFGEN_HIP_ENODEV, "ngpu = %d but only %d HIP device(s) visible", ngpu, ndev);
+    if (want > 1 && nk >= 4) {
+        const int n = std::min(want, nk / 2);
         return run_zslab_local(tri, ntri, xyz, nvert, origin, dx, ni, nj, nk, exact_band, n, out_layout, phi_out,
                                err);
     }

@@ -1,11 +1,19 @@
-// sdfgen_unified.cpp -- sdfgen::make_level_set3 / is_gpu_available on top of the C-ABIs.
-// Mirrors /root/reference/common/sdfgen_unified.cpp:19-71 (dispatch), with the
-// GPU case served by sdfgen_hip_make_level_set3 and errors thrown instead of exit().
+// sdfgen_unified.cpp -- the reference's C++ entry points on top of the C-ABIs:
+//   sdfgen::make_level_set3 / is_gpu_available   common/sdfgen_unified.h:47-57, 68 (dispatch
+//                                                 as common/sdfgen_unified.cpp:19-71)
+//   sdfgen::gpu::make_level_set3                  gpu_lib/makelevelset3_gpu.h:40-42
+//   sdfgen::cpu::make_level_set3                  cpu_lib/makelevelset3.h:39-41
+// The GPU case is served by sdfgen_hip_make_level_set3 (hand-written gfx950 kernels), the
+// CPU case by sdfgen_cpu_make_level_set3; errors are thrown, never exit().  The types are the
+// reference's (include/sdfgen/{vec,array1,array3}.h), so these four symbols are the ones a
+// reference caller's object files import.
 #include "sdfgen/sdfgen_unified.h"
 
 #include <stdexcept>
 #include <string>
 
+#include "sdfgen/makelevelset3.h"
+#include "sdfgen/makelevelset3_gpu.h"
 #include "sdfgen_cpu.h"
 #include "sdfgen_hip.h"
 
@@ -13,7 +21,9 @@ namespace sdfgen {
 
 bool is_gpu_available() { return sdfgen_hip_device_count() > 0; }
 
-static void throw_for(int rc, const char *msg)
+namespace {
+
+void throw_for(int rc, const char *msg)
 {
     std::string m(msg && *msg ? msg : "SDF generation failed");
     if (rc == SDFGEN_HIP_EINVAL) throw std::invalid_argument(m);
@@ -21,27 +31,60 @@ static void throw_for(int rc, const char *msg)
     throw std::runtime_error(m);
 }
 
+// Validate dims and size the caller's Array3f (the callee resizes it, cpu_lib/makelevelset3.cpp:196).
+void prepare(int nx, int ny, int nz, Array3f &phi)
+{
+    if (nx <= 0 || ny <= 0 || nz <= 0) throw std::invalid_argument("Grid dimensions must be positive");
+    phi.resize(nx, ny, nz);
+}
+
+const uint32_t *tri_ptr(const std::vector<Vec3ui> &tri)
+{
+    return tri.empty() ? nullptr : reinterpret_cast<const uint32_t *>(tri.data());  // packed uint32[n][3]
+}
+const float *xyz_ptr(const std::vector<Vec3f> &x)
+{
+    return x.empty() ? nullptr : reinterpret_cast<const float *>(x.data());  // packed float[n][3]
+}
+
+}  // namespace
+
+namespace gpu {
+void make_level_set3(const std::vector<Vec3ui> &tri, const std::vector<Vec3f> &x, const Vec3f &origin, float dx,
+                     int nx, int ny, int nz, Array3f &phi, const int exact_band)
+{
+    if (!is_gpu_available())
+        throw std::runtime_error("GPU backend requested but no HIP GPU is available. Use HardwareBackend::CPU.");
+    prepare(nx, ny, nz, phi);
+    char err[512] = {0};
+    const float o[3] = {origin[0], origin[1], origin[2]};
+    const int rc = sdfgen_hip_make_level_set3(tri_ptr(tri), tri.size(), xyz_ptr(x), x.size(), o, dx, nx, ny, nz,
+                                              exact_band, SDFGEN_NGPU_CURRENT, SDFGEN_LAYOUT_ARRAY3, phi.a.data, err,
+                                              sizeof(err));
+    if (rc != 0) throw_for(rc, err);
+}
+}  // namespace gpu
+
+namespace cpu {
+void make_level_set3(const std::vector<Vec3ui> &tri, const std::vector<Vec3f> &x, const Vec3f &origin, float dx,
+                     int nx, int ny, int nz, Array3f &phi, const int exact_band, int num_threads)
+{
+    prepare(nx, ny, nz, phi);
+    char err[512] = {0};
+    const float o[3] = {origin[0], origin[1], origin[2]};
+    const int rc = sdfgen_cpu_make_level_set3(tri_ptr(tri), tri.size(), xyz_ptr(x), x.size(), o, dx, nx, ny, nz,
+                                              exact_band, num_threads, SDFGEN_LAYOUT_ARRAY3, phi.a.data, err,
+                                              sizeof(err));
+    if (rc != 0) throw_for(rc, err);
+}
+}  // namespace cpu
+
 void make_level_set3(const std::vector<Vec3ui> &tri, const std::vector<Vec3f> &x, const Vec3f &origin, float dx,
                      int nx, int ny, int nz, Array3f &phi, int exact_band, HardwareBackend backend, int num_threads)
 {
     if (backend == HardwareBackend::Auto) backend = is_gpu_available() ? HardwareBackend::GPU : HardwareBackend::CPU;
-    if (nx <= 0 || ny <= 0 || nz <= 0) throw std::invalid_argument("Grid dimensions must be positive");
-    phi.resize(nx, ny, nz);
-    char err[512] = {0};
-    const float o[3] = {origin[0], origin[1], origin[2]};
-    const uint32_t *t = tri.empty() ? nullptr : reinterpret_cast<const uint32_t *>(tri.data());
-    const float *v = x.empty() ? nullptr : reinterpret_cast<const float *>(x.data());
-    int rc;
-    if (backend == HardwareBackend::GPU) {
-        if (!is_gpu_available())
-            throw std::runtime_error("GPU backend requested but no HIP GPU is available. Use HardwareBackend::CPU.");
-        rc = sdfgen_hip_make_level_set3(t, tri.size(), v, x.size(), o, dx, nx, ny, nz, exact_band, 0,
-                                        SDFGEN_LAYOUT_ARRAY3, phi.data(), err, sizeof(err));
-    } else {
-        rc = sdfgen_cpu_make_level_set3(t, tri.size(), v, x.size(), o, dx, nx, ny, nz, exact_band, num_threads, 0,
-                                        phi.data(), err, sizeof(err));
-    }
-    if (rc != 0) throw_for(rc, err);
+    if (backend == HardwareBackend::GPU) gpu::make_level_set3(tri, x, origin, dx, nx, ny, nz, phi, exact_band);
+    else cpu::make_level_set3(tri, x, origin, dx, nx, ny, nz, phi, exact_band, num_threads);
 }
 
 }  // namespace sdfgen

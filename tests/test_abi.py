@@ -70,3 +70,9 @@ def test_no_oracle_in_product_library():
     assert "oracle" not in out
     deps = subprocess.run(["ldd", _lib.LIB_PATH], capture_output=True, text=True).stdout
     assert "oracle" not in deps and "sdfref" not in deps
+
+
+def test_negative_ngpu_is_einval():
+    v, t = np.eye(3, dtype=np.float32), np.array([[0, 1, 2]], np.uint32)
+    with pytest.raises(ValueError, match="ngpu"):
+        _lib.make_level_set3(v, t, (0, 0, 0), 0.1, 4, 4, 4, ngpu=-1)

@@ -163,3 +163,17 @@ def test_c_abi_ngpu_more_than_visible_is_enodev():
     v, t, o, dx, dims = _mesh(dims=(20, 20, 20))
     with pytest.raises(RuntimeError, match="visible"):
         _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_KFAST, ngpu=n + 1)
+
+
+def test_c_abi_ngpu_all_means_every_visible_device():
+    """ngpu = SDFGEN_NGPU_ALL (0) = all visible devices; on a one-GPU box that
+    is the single-device run, bit-exact like ngpu = SDFGEN_NGPU_CURRENT (1)."""
+    from sdfgenfast_amd import _lib
+    v, t, o, dx, dims = _mesh(dims=(24, 20, 28))
+    want = O.make_level_set3(v, t, o, dx, *dims, 1)
+    got_all = _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_KFAST, ngpu=_lib.NGPU_ALL)
+    got_cur = _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_KFAST, ngpu=_lib.NGPU_CURRENT)
+    assert bits_equal(got_all, want), diff_report(got_all, want, dx)
+    assert bits_equal(got_cur, want), diff_report(got_cur, want, dx)
+    if _lib.device_count() == 1:
+        assert _lib.last_profile()["sweep_impl"] != 3  # one device: not the slab path
