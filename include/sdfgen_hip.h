@@ -36,7 +36,7 @@ extern "C" {
 /* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
 #pragma GCC visibility push(default)
 
-#define SDFGEN_HIP_ABI_VERSION 1
+#define SDFGEN_HIP_ABI_VERSION 2   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare */
 
 enum {
     SDFGEN_HIP_OK = 0,
@@ -108,8 +108,8 @@ typedef struct sdfgen_hip_profile {
     double sweep_launch_ms[16];  /* per (pass, direction) sweep */
     int sweep_launches;       /* kernel launches issued for the sweeps */
     int sweep_impl;           /* 0 = hyperplane launches, 1 = pipelined 8x8-tile column wavefront,
-                                 2 = tile wavefront for the first pass + Jacobi/repair for sparse sweeps,
-                                 3 = Z-slab tile wavefront (sdfgen_hip_slab_*) */
+                                 2 = tile wavefront for the first pass + Jacobi/repair for sparse sweeps
+                                 (on one device or, `slabs` > 1, per Z-slab) */
     uint64_t band_evals;      /* point-triangle evaluations in the band phase */
     uint64_t sweep_evals;     /* evaluations in the sweeps (0 unless SDFGEN_COUNT_EVALS is set) */
     uint64_t sweep_stalls;    /* compute-wave polls that found a hand-off not yet landed (same) */
@@ -121,7 +121,9 @@ typedef struct sdfgen_hip_profile {
     uint64_t sparse_claims;   /* rechecks run depth-first by the lane that requested them */
     int tile_multi;           /* first-pass sweeps run as ONE overlapped launch (0: one launch per
                                  sweep); its time is then sweep_launch_ms[0] */
-    int reserved_;
+    int slabs;                /* Z-slabs the grid was split into (0 or 1: one device) */
+    double chain_steps;       /* modelled critical path of the first-pass launch, in tile steps (the
+                                 latency roofline's chain length; 0 without the overlapped launch) */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
@@ -158,6 +160,10 @@ int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *s, const void *lower, const voi
                                 size_t errlen);
 int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *s, sdfgen_hip_slab *lower, sdfgen_hip_slab *upper,
                                   char *errbuf, size_t errlen);
+/* Allocate everything a call with ntri triangles needs (enqueue does it too when needed).  A
+ * thread that drives SEVERAL slabs must prepare all of them before it enqueues any of them: setting
+ * a slab up while another slab's kernels already wait on it can block the thread. */
+int sdfgen_hip_slab_prepare(sdfgen_hip_slab *s, uint64_t ntri, char *errbuf, size_t errlen);
 /* Device buffers on the session's GPU; d_phi_slab receives ni*nj*(k_end-k_begin) floats in
  * the chosen layout (ARRAY3: i fastest, the slab's planes only; KFAST: k fastest). */
 int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *s, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
@@ -170,6 +176,10 @@ int sdfgen_hip_slab_run(sdfgen_hip_slab *s, const uint32_t *tri, uint64_t ntri, 
                         const float origin[3], float dx, int exact_band, int out_layout, float *phi_slab,
                         sdfgen_hip_profile *prof, char *errbuf, size_t errlen);
 int sdfgen_hip_slab_destroy(sdfgen_hip_slab *s);
+/* Diagnostics: copy a slab's device state to host (after its stream drained).  which: 0 = the
+ * communication block, 1 = tile-sweep control words, 2 = first-pass completion flags, 3 = its
+ * task table, 4 = its dependency table.  *n_bytes = bytes copied (at most max_bytes). */
+int sdfgen_hip_slab_debug_dump(sdfgen_hip_slab *s, int which, void *out, uint64_t max_bytes, uint64_t *n_bytes);
 
 /* Diagnostics (used by the parity tests): evaluate the device geometry kernels
  * on host arrays.  pts: n x 12 floats (x0,x1,x2,x3) -> out: n floats;

@@ -44,12 +44,18 @@ EXPORTED = (
     "sdfgen_hip_slab_finish",
     "sdfgen_hip_slab_run",
     "sdfgen_hip_slab_destroy",
+    "sdfgen_hip_slab_prepare",
+    "sdfgen_hip_slab_debug_dump",
     "sdfgen_cpu_slab_create",
     "sdfgen_cpu_slab_range",
     "sdfgen_cpu_slab_band",
     "sdfgen_cpu_slab_sweep",
     "sdfgen_cpu_slab_sign",
     "sdfgen_cpu_slab_destroy",
+    "sdfgen_mesh_load",
+    "sdfgen_mesh_info",
+    "sdfgen_mesh_copy",
+    "sdfgen_mesh_free",
 )
 IPC_HANDLE_BYTES = 64
 
@@ -74,7 +80,8 @@ class Profile(ctypes.Structure):
         ("sparse_rechecks", ctypes.c_uint64),
         ("sparse_claims", ctypes.c_uint64),
         ("tile_multi", ctypes.c_int),
-        ("reserved_", ctypes.c_int),
+        ("slabs", ctypes.c_int),
+        ("chain_steps", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -124,7 +131,10 @@ def _load():
     L.sdfgen_hip_slab_run.argtypes = [_P, _P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int, _P,
                                       ctypes.POINTER(Profile)] + _E
     L.sdfgen_hip_slab_destroy.argtypes = [_P]
-    for f in ("create", "range", "export", "connect_ipc", "connect_local", "enqueue", "finish", "run", "destroy"):
+    L.sdfgen_hip_slab_debug_dump.argtypes = [_P, ctypes.c_int, _P, _u64, ctypes.POINTER(_u64)]
+    L.sdfgen_hip_slab_prepare.argtypes = [_P, _u64] + _E
+    for f in ("create", "range", "export", "connect_ipc", "connect_local", "enqueue", "finish", "run", "destroy",
+              "debug_dump", "prepare"):
         getattr(L, "sdfgen_hip_slab_" + f).restype = ctypes.c_int
     L.sdfgen_cpu_slab_create.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(_P)] + _E
     L.sdfgen_cpu_slab_range.argtypes = [_P, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
@@ -134,6 +144,12 @@ def _load():
     L.sdfgen_cpu_slab_destroy.argtypes = [_P]
     for f in ("create", "range", "band", "sweep", "sign", "destroy"):
         getattr(L, "sdfgen_cpu_slab_" + f).restype = ctypes.c_int
+    L.sdfgen_mesh_load.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_P)] + _E
+    L.sdfgen_mesh_info.argtypes = [_P, ctypes.POINTER(_u64), ctypes.POINTER(_u64), _P, ctypes.POINTER(ctypes.c_int)]
+    L.sdfgen_mesh_copy.argtypes = [_P, _P, _P]
+    L.sdfgen_mesh_free.argtypes = [_P]
+    for f in ("load", "info", "copy", "free"):
+        getattr(L, "sdfgen_mesh_" + f).restype = ctypes.c_int
     return L
 
 
@@ -157,19 +173,49 @@ def _raise(code: int, buf) -> None:
     raise HipError(code, msg or f"GPU (HIP) backend error {code}")
 
 
+MESH_AUTO, MESH_OBJ, MESH_STL, MESH_STL_BINARY, MESH_STL_ASCII = 0, 1, 2, 3, 4
+
+
+def mesh_load(path: str, fmt: int = MESH_AUTO):
+    """Native mesh loader (include/sdfgen_meshio.h) -> (vertices (n,3) f32, triangles (m,3) u32,
+    bounds (min xyz, max xyz) as float32, detected format).  Raises RuntimeError on failure,
+    like the reference's loaders returning false (common/mesh_io.cpp:29-48)."""
+    h = _P()
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_mesh_load(os.fsencode(path), int(fmt), ctypes.byref(h), err, ctypes.sizeof(err))
+    if rc != OK:
+        raise RuntimeError(err.value.decode(errors="replace") or f"Failed to load mesh: {path}")
+    try:
+        nv, nt, f = _u64(), _u64(), ctypes.c_int()
+        b = np.empty(6, np.float32)
+        lib.sdfgen_mesh_info(h, ctypes.byref(nv), ctypes.byref(nt), b.ctypes.data_as(_P), ctypes.byref(f))
+        v = np.empty((nv.value, 3), np.float32)
+        t = np.empty((nt.value, 3), np.uint32)
+        lib.sdfgen_mesh_copy(h, v.ctypes.data_as(_P), t.ctypes.data_as(_P))
+    finally:
+        lib.sdfgen_mesh_free(h)
+    return v, t, b, f.value
+
+
 def device_count() -> int:
     return int(lib.sdfgen_hip_device_count())
 
 
 def make_level_set3(vertices: np.ndarray, triangles: np.ndarray, origin, dx: float, ni: int, nj: int, nk: int,
-                    exact_band: int = 1, layout: int = LAYOUT_KFAST, ngpu: int = 1) -> np.ndarray:
+                    exact_band: int = 1, layout: int = LAYOUT_KFAST, ngpu: int = 1,
+                    out: np.ndarray | None = None) -> np.ndarray:
     """Host-memory entry (sdfgen_hip_make_level_set3).  Returns phi as a (ni,nj,nk)
     array: C-ordered for LAYOUT_KFAST, a Fortran-ordered view of the i-fastest
-    Array3f buffer for LAYOUT_ARRAY3 -- either way phi[i, j, k]."""
+    Array3f buffer for LAYOUT_ARRAY3 -- either way phi[i, j, k].  `out`: an optional
+    contiguous float32 buffer of ni*nj*nk elements to write into (reused across calls)."""
     v = np.ascontiguousarray(vertices, dtype=np.float32)
     t = np.ascontiguousarray(triangles, dtype=np.uint32)
     o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
-    out = np.empty(int(ni) * int(nj) * int(nk), dtype=np.float32)
+    if out is None:
+        out = np.empty(int(ni) * int(nj) * int(nk), dtype=np.float32)
+    elif out.dtype != np.float32 or out.size != int(ni) * int(nj) * int(nk) or not out.flags.c_contiguous:
+        raise ValueError("out must be a C-contiguous float32 array of ni*nj*nk elements")
+    out = out.reshape(-1)
     err = ctypes.create_string_buffer(512)
     rc = lib.sdfgen_hip_make_level_set3(t.ctypes.data_as(_P), t.shape[0] if t.ndim == 2 else t.size // 3,
                                         v.ctypes.data_as(_P), v.shape[0] if v.ndim == 2 else v.size // 3,
@@ -294,6 +340,12 @@ class Slab:
         self._check(lib.sdfgen_hip_slab_connect_local(self.h, lower.h if lower else None, upper.h if upper else None,
                                                       err, ctypes.sizeof(err)), err)
 
+    def prepare(self, ntri: int) -> None:
+        """Allocate for a call with ntri triangles; with several slabs in one thread, prepare
+        every slab before enqueuing any (sdfgen_hip_slab_prepare)."""
+        err = ctypes.create_string_buffer(512)
+        self._check(lib.sdfgen_hip_slab_prepare(self.h, int(ntri), err, ctypes.sizeof(err)), err)
+
     def enqueue(self, d_tri: int, ntri: int, d_xyz: int, nvert: int, origin, dx: float, exact_band: int,
                 layout: int, d_out: int) -> None:
         o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
@@ -325,6 +377,16 @@ class Slab:
         if layout == LAYOUT_KFAST:
             return out.reshape((ni, nj, nks)), p.as_dict()
         return out.reshape((ni, nj, nks), order="F"), p.as_dict()
+
+    def debug_dump(self, which: int, max_bytes: int = 1 << 26) -> bytes:
+        """Diagnostics (sdfgen_hip_slab_debug_dump): 0 comm block, 1 tile control words,
+        2 first-pass completion flags, 3 task table, 4 dependency table."""
+        buf = ctypes.create_string_buffer(max_bytes)
+        n = _u64()
+        rc = lib.sdfgen_hip_slab_debug_dump(self.h, int(which), buf, max_bytes, ctypes.byref(n))
+        if rc != OK:
+            raise HipError(rc, "debug dump failed")
+        return buf.raw[:n.value]
 
     def close(self) -> None:
         if getattr(self, "h", None):

@@ -41,6 +41,24 @@ SDF_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
 constexpr uint32_t LBL_BITS = 27u, LBL_MASK = (1u << LBL_BITS) - 1u;
 SDF_HD int lbl_of(uint32_t w) { const uint32_t l = w & LBL_MASK; return l == LBL_MASK ? -1 : (int)l; }
 SDF_HD int lc_of(uint32_t w) { return (int)(w >> LBL_BITS); }
+// Debug builds (make BOUNDS=1 -> -DSDFGEN_BOUNDS): every global index the sweep kernels form
+// is checked against the buffer it addresses; the first violation is recorded as
+// (site << 48 | index) in sdf_oob and the access is redirected to `lo`, so a bad index is
+// reported by the host (sdfgen_hip.hip: check_oob) instead of faulting the GPU.
+#ifdef SDFGEN_BOUNDS
+static __device__ unsigned long long sdf_oob;
+__device__ __forceinline__ unsigned long long sdf_chk(unsigned site, unsigned long long x, unsigned long long lo,
+                                                      unsigned long long hi)
+{
+    if (x >= lo && x < hi) return x;
+    atomicCAS(&sdf_oob, 0ull, ((unsigned long long)site << 48) | (x & 0xffffffffffffull));
+    return lo;
+}
+#define SDF_CHK(site, x, lo, hi) sdf_chk((site), (unsigned long long)(x), (unsigned long long)(lo), (unsigned long long)(hi))
+#else
+#define SDF_CHK(site, x, lo, hi) (x)
+#endif
+
 SDF_HD uint32_t lo_word(int label, int lc) { return ((uint32_t)lc << LBL_BITS) | ((uint32_t)label & LBL_MASK); }
 SDF_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 

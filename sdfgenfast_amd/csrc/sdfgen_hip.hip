@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <vector>
 
@@ -361,27 +362,28 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
                                               int layout, float *__restrict__ out, int k_lo, int k_cnt)
 {
     const int lane = threadIdx.x & 63;
-    const uint64_t row = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
     const uint64_t nrows = (uint64_t)g.nj * k_cnt;
-    if (row >= nrows) return;
-    const int j = (int)(row % g.nj), k = k_lo + (int)(row / g.nj);
-    const size_t base = cidx(0, j, k, g.ni, g.nj);
-    uint32_t carry = 0;
-    for (int i0 = 0; i0 < g.ni; i0 += 64) {
-        const int i = i0 + lane;
-        const bool ok = i < g.ni;
-        uint32_t par = ok ? (cnt[base + i] & 1u) : 0u;
-        const u64 mask = __ballot(par);
-        const u64 below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);  // lanes 0..lane
-        const uint32_t pre = (carry + (uint32_t)__popcll(mask & below)) & 1u;
-        if (ok) {
-            uint32_t bits = (uint32_t)(cell[base + i] >> 32);
-            if (pre) bits ^= 0x80000000u;
-            float v = __uint_as_float(bits);
-            if (layout == SDFGEN_LAYOUT_ARRAY3) out[cidx(i, j, k - k_lo, g.ni, g.nj)] = v;
-            else out[((size_t)i * g.nj + j) * k_cnt + (k - k_lo)] = v;
+    const uint64_t rstep = ((uint64_t)gridDim.x * blockDim.x) >> 6;   // grid-stride over rows (capped grid)
+    for (uint64_t row = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6; row < nrows; row += rstep) {
+        const int j = (int)(row % g.nj), k = k_lo + (int)(row / g.nj);
+        const size_t base = cidx(0, j, k, g.ni, g.nj);
+        uint32_t carry = 0;
+        for (int i0 = 0; i0 < g.ni; i0 += 64) {
+            const int i = i0 + lane;
+            const bool ok = i < g.ni;
+            uint32_t par = ok ? (cnt[base + i] & 1u) : 0u;
+            const u64 mask = __ballot(par);
+            const u64 below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);  // lanes 0..lane
+            const uint32_t pre = (carry + (uint32_t)__popcll(mask & below)) & 1u;
+            if (ok) {
+                uint32_t bits = (uint32_t)(cell[base + i] >> 32);
+                if (pre) bits ^= 0x80000000u;
+                float v = __uint_as_float(bits);
+                if (layout == SDFGEN_LAYOUT_ARRAY3) out[cidx(i, j, k - k_lo, g.ni, g.nj)] = v;
+                else out[((size_t)i * g.nj + j) * k_cnt + (k - k_lo)] = v;
+            }
+            carry = (carry + (uint32_t)__popcll(mask)) & 1u;
         }
-        carry = (carry + (uint32_t)__popcll(mask)) & 1u;
     }
 }
 
@@ -517,6 +519,24 @@ inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap)
     return (unsigned)b;
 }
 
+// Bounds-checked builds (make BOUNDS=1): report the first out-of-range index a kernel formed.
+int check_oob(Err &err, const char *where)
+{
+#ifdef SDFGEN_BOUNDS
+    unsigned long long v = 0, z = 0;
+    HIPCHK(hipMemcpyFromSymbol(&v, HIP_SYMBOL(sdf_oob), sizeof(v)));
+    if (v) {
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(sdf_oob), &z, sizeof(z)));
+        return err.set(SDFGEN_HIP_ERUNTIME, "%s: out-of-range index at site %llu: %llu", where, v >> 48,
+                       v & 0xffffffffffffull);
+    }
+#else
+    (void)err;
+    (void)where;
+#endif
+    return 0;
+}
+
 // The whole pipeline on device buffers already resident on ws->device.
 int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
                  uint64_t nvert, const float origin[3], float dx, int ni, int nj, int nk, int band, int layout,
@@ -589,6 +609,10 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->sp.workers = e ? atoi(e) : (n <= (1ull << 25) ? 64 : SP_WORKERS_DEFAULT);
     }
     ws->wf.skip_seen = getenv("SDFGEN_NO_SEEN_SKIP") == nullptr;   // diagnostics
+    ws->wf.clo = 0;
+    ws->wf.chi = n;
+    ws->wf.ntri = ntri;
+    ws->sp.ntri = ntri;
     if (ws->wf.ctrl) HIPCHK(hipMemsetAsync(ws->wf.ctrl + 1, 0, sizeof(int), st));   // error bits of this call
     if (sparse_first < 16 && ws->sp.ctl) HIPCHK(hipMemsetAsync(ws->sp.ctl, 0, SP_NCTL * sizeof(u64), st));
     // The first pass's tile sweeps as ONE launch whose sweeps overlap (tile_sweep_multi) unless
@@ -649,7 +673,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipEventRecord(ev[19], st));
     {
         const uint64_t rows = (uint64_t)nj * nk;
-        hipLaunchKernelGGL(k_sign, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, st, ws->cell, ws->cnt, g,
+        hipLaunchKernelGGL(k_sign, dim3(grid_for(rows * 64, 256, 65536)), dim3(256), 0, st, ws->cell, ws->cnt, g,
                            layout, d_out, 0, nk);
         HIPCHK(hipGetLastError());
     }
@@ -666,6 +690,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipMemcpyAsync(&evals, ws->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     HIPCHK(hipGetLastError());
+    if ((rc = check_oob(err, "make_level_set3"))) return rc;
 
     sdfgen_hip_profile p;
     memset(&p, 0, sizeof(p));
@@ -693,6 +718,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.own_waits = wf_stats[3];
     p.sparse_sweeps = sparse_sweeps;
     p.tile_multi = multi_n;
+    p.chain_steps = multi_n > 1 ? ws->wf.chain_steps : 0.0;
+    p.slabs = 1;
     p.sparse_first = sparse_sweeps ? sparse_first : 16;
 #ifdef SP_JACOBI_COUNT
     fprintf(stderr, "jacobi candidates %llu lane-passes %llu (slot use %.3f)\n", sp_ctl[SP_DIAG], sp_ctl[SP_DIAG + 1],
@@ -725,51 +752,111 @@ int device_count_impl()
 // Z-slab sessions: one slab of k planes per GPU (one process per GPU, or several
 // slabs in one process).  DESIGN.md §7.
 //   * band, ray parity, sign: local to the slab (boxes clamped to the whole grid first);
-//   * each sweep: the tile wavefront runs over this slab's oriented c range; the plane
-//     just upstream arrives as tagged granules in an inbox written by the upstream GPU
-//     (over xGMI, IPC-mapped), and this slab's last plane is written into the
-//     downstream GPU's inbox -- the wavefront pipelines straight across GPUs.
-//   * inboxes alternate by sweep parity: consecutive sweeps in the same k direction
-//     (3,4 / 1,2 / ...) never share a buffer, and a producer cannot start the sweep
-//     after next before its consumer finished reading (it needs that consumer's
-//     granules in between).
+//   * first pass (sweeps 1-8): the tile wavefront over this slab's oriented c range, all eight
+//     sweeps in ONE overlapped launch scheduled for the whole grid (tile_sweep_multi); the plane
+//     just upstream arrives as tagged granules in a per-sweep inbox written by the upstream GPU
+//     (xGMI, IPC- or peer-mapped), and this slab's last plane is written into the downstream
+//     GPU's inbox -- the wavefront pipelines straight across GPUs;
+//   * second pass (sweeps 9-16): Jacobi + change-driven repair per slab (sweep_sparse.hpp); the
+//     neighbour planes are kept in halo planes, changes of a boundary plane are pushed to the
+//     neighbour (with a recheck request for the downstream one), and a neighbour handshake
+//     (DONE / READY flags) separates the sweeps.
+// Everything a neighbour writes lives in ONE uncached block per slab (`comm`), exported once.
 // ---------------------------------------------------------------------------
+struct CommLayout {
+    size_t plane = 0;            // cells per plane (ni * nj)
+    size_t ring_cap = 0;         // inbound ring entries per side
+    size_t off_halo = 0, off_ring = 0, off_flags = 0, bytes = 0;
+    void init(size_t plane_cells)
+    {
+        plane = plane_cells;
+        ring_cap = 4 * plane + 4096;   // boundary relabels per sweep (error bit 8 beyond)
+        off_halo = 8 * plane * sizeof(u64);                        // 8 per-sweep tile inboxes
+        off_ring = off_halo + 4 * plane * sizeof(uint32_t);        // halo planes [side][parity]
+        off_flags = (off_ring + 2 * ring_cap * sizeof(uint32_t) + 127) / 128 * 128;
+        const size_t raw = off_flags + SP_FL_WORDS * SP_FL_STRIDE * sizeof(u64);
+        bytes = (raw + (2u << 20) - 1) / (2u << 20) * (2u << 20);  // whole 2 MiB: a dedicated allocation
+    }
+    u64 *inbox(char *base, int sweep) const { return (u64 *)base + plane * (size_t)(sweep % 8); }
+    uint32_t *halo(char *base, int side, int par) const { return (uint32_t *)(base + off_halo) + plane * (size_t)(2 * side + par); }
+    uint32_t *ring(char *base, int side) const { return (uint32_t *)(base + off_ring) + ring_cap * (size_t)side; }
+    u64 *flags(char *base) const { return (u64 *)(base + off_flags); }
+};
+
 struct SlabSession {
     int device = -1, nslabs = 1, slab = 0, ni = 0, nj = 0, nk = 0, k_begin = 0, k_end = 0;
     hipStream_t stream = nullptr;
-    u64 *cell = nullptr;
-    uint32_t *cnt = nullptr;
+    // Cell state of this slab's planes only (k in [k_begin, k_end)): cell_mem holds them, and
+    // cell = cell_mem - k_begin * ni * nj so the kernels index it with global cell numbers
+    // (every kernel of a slab touches only its own planes; the neighbour planes arrive through
+    // the inboxes and halo planes).  Same for cnt and the sparse pass's second buffer alt.
+    u64 *cell = nullptr, *cell_mem = nullptr, *alt = nullptr, *alt_mem = nullptr;
+    uint32_t *cnt = nullptr, *cnt_mem = nullptr;
     float4 *soup = nullptr;
     uint32_t *tri = nullptr;
     float *xyz = nullptr, *out = nullptr;
     int *err_flag = nullptr;
+    unsigned *arrive = nullptr;
     unsigned long long *evals = nullptr;
     size_t cap_soup = 0, cap_tri = 0, cap_xyz = 0, cap_out = 0;
     TileSweepWorkspace wf;
-    u64 *inbox_mem = nullptr;   // 4 planes: [from lower (dk>0)][parity], [from upper (dk<0)][parity]
-    size_t plane = 0;           // granules per plane: (ni) x (nj)  -- a, b in [-1, A) x [-1, B)
-    u64 *peer_lower = nullptr, *peer_upper = nullptr;   // neighbours' inbox_mem (mapped)
-    bool lower_ipc = false, upper_ipc = false;
+    SparseSweepWorkspace sp;
+    CommLayout cl;
+    char *comm = nullptr;          // uncached, IPC-exported: inboxes, halo planes, inbound rings, flags
+    char *peer[2] = {nullptr, nullptr};   // the lower / upper neighbour's comm (mapped)
+    bool peer_ipc[2] = {false, false};
+    unsigned long long sync_epoch = 0;    // neighbour handshakes issued (same count on every slab)
+    uint64_t prepared_ntri = ~0ull;       // slab_prepare was run for this many triangles
+    int sparse_sweeps = 0, tile_multi = 0;
     hipEvent_t ev[24] = {};
     int launches = 0;
     std::mutex mu;
-
-    u64 *inbox(int from_upper, int parity) const { return inbox_mem + plane * (2 * from_upper + parity); }
 };
+
+// Resolve every kernel a slab launches before any of its work is enqueued.  A kernel's first
+// launch makes the HIP runtime load it (deferred code-object loading); doing that while this
+// process's other slabs already run kernels that wait on work not yet enqueued has been seen to
+// block the enqueuing thread -- the in-process multi-slab path deadlocked until a watchdog fired
+// (DESIGN.md §7).  hipFuncGetAttributes loads the kernel without launching it.
+int slab_preload_kernels(Err &err)
+{
+    if (getenv("SDFGEN_NO_KERNEL_PRELOAD")) return 0;   // diagnostics
+    const void *k[] = {(const void *)k_prep_soup, (const void *)k_init, (const void *)k_band_lds,
+                       (const void *)k_sign, (const void *)k_sweep_tile<true, false, false>,
+                       (const void *)k_sweep_tile<true, false, true>, (const void *)k_sp_jacobi<true>,
+                       (const void *)k_sp_jlist<true>, (const void *)k_sp_recheck<true>, (const void *)k_sp_slab_wait,
+                       (const void *)k_sp_slab_halo, (const void *)k_sp_slab_export};
+    for (const void *f : k) {
+        hipFuncAttributes a;
+        HIPCHK(hipFuncGetAttributes(&a, f));
+    }
+    return 0;
+}
 
 int slab_alloc(SlabSession *S, Err &err)
 {
     HIPCHK(hipSetDevice(S->device));
+    if (int rc = slab_preload_kernels(err)) return rc;
     HIPCHK(hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
     for (auto &e : S->ev) HIPCHK(hipEventCreate(&e));
-    const uint64_t n = (uint64_t)S->ni * S->nj * S->nk;
-    HIPCHK(hipMalloc((void **)&S->cell, n * sizeof(u64)));
-    HIPCHK(hipMalloc((void **)&S->cnt, n * sizeof(uint32_t)));
+    const size_t plane = (size_t)S->ni * S->nj;
+    const uint64_t n = plane * (uint64_t)(S->k_end - S->k_begin);   // this slab's planes only
+    HIPCHK(hipMalloc((void **)&S->cell_mem, n * sizeof(u64)));
+    HIPCHK(hipMalloc((void **)&S->cnt_mem, n * sizeof(uint32_t)));
+    S->cell = S->cell_mem - plane * (size_t)S->k_begin;
+    S->cnt = S->cnt_mem - plane * (size_t)S->k_begin;
     HIPCHK(hipMalloc((void **)&S->err_flag, sizeof(int)));
     HIPCHK(hipMalloc((void **)&S->evals, sizeof(unsigned long long)));
-    S->plane = (size_t)S->ni * S->nj;
-    HIPCHK(hipMalloc((void **)&S->inbox_mem, 4 * S->plane * sizeof(u64)));
-    HIPCHK(hipMemset(S->inbox_mem, 0, 4 * S->plane * sizeof(u64)));   // epoch 0 is never published
+    HIPCHK(hipMalloc((void **)&S->arrive, sizeof(unsigned)));
+    // The communication block is written by the NEIGHBOUR GPUs (system-scope stores over xGMI,
+    // through an IPC or peer mapping) while this GPU's kernels poll it.  Plain hipMalloc memory
+    // is coarse-grained: HIP makes remote writes to it visible only at kernel boundaries (an L2
+    // of this GPU may keep serving a stale line).  Uncached device memory (MTYPE UC) is held in
+    // no cache, so every system-scope load of a poll reads what the remote system-scope store
+    // wrote, mid-kernel.  Whole 2 MiB: a dedicated allocation that IPC maps as is.
+    S->cl.init(plane);
+    HIPCHK(hipExtMallocWithFlags((void **)&S->comm, S->cl.bytes, hipDeviceMallocUncached));
+    HIPCHK(hipMemset(S->comm, 0, S->cl.bytes));   // epoch 0 is never published, flags start at 0
     HIPCHK(hipDeviceSynchronize());
     return 0;
 }
@@ -779,42 +866,82 @@ void slab_free(SlabSession *S)
     if (S->device < 0) return;
     (void)hipSetDevice(S->device);
     if (S->stream) (void)hipStreamSynchronize(S->stream);
-    if (S->lower_ipc && S->peer_lower) (void)hipIpcCloseMemHandle(S->peer_lower);
-    if (S->upper_ipc && S->peer_upper) (void)hipIpcCloseMemHandle(S->peer_upper);
-    (void)hipFree(S->cell);
-    (void)hipFree(S->cnt);
+    for (int side = 0; side < 2; ++side)
+        if (S->peer_ipc[side] && S->peer[side]) (void)hipIpcCloseMemHandle(S->peer[side]);
+    (void)hipFree(S->cell_mem);
+    (void)hipFree(S->alt_mem);
+    (void)hipFree(S->cnt_mem);
     (void)hipFree(S->soup);
     (void)hipFree(S->tri);
     (void)hipFree(S->xyz);
     (void)hipFree(S->out);
     (void)hipFree(S->err_flag);
     (void)hipFree(S->evals);
-    (void)hipFree(S->inbox_mem);
+    (void)hipFree(S->arrive);
+    (void)hipFree(S->comm);
     tile_sweep_release(S->wf);
+    sparse_sweep_release(S->sp);
     for (auto &e : S->ev)
         if (e) (void)hipEventDestroy(e);
     if (S->stream) (void)hipStreamDestroy(S->stream);
 }
 
 // Oriented c range of this slab for a sweep with k direction dk (see sweep_tile.hpp).
-void slab_c_range(const SlabSession *S, int dk, int *cs, int *ce)
+void slab_c_range(const SlabSession *S, int dk, int *cs, int *ce) { st_slab_c_range(S->k_begin, S->k_end, S->nk, dk, cs, ce); }
+
+// Upstream / downstream neighbour side of a sweep: 0 = lower slab, 1 = upper slab (-1: none).
+int slab_up_side(const SlabSession *S, int dk)
 {
-    if (dk > 0) {
-        *cs = std::max(S->k_begin, 1) - 1;
-        *ce = S->k_end - 1;
-    } else {
-        *cs = S->nk - 1 - std::min(S->k_end, S->nk - 1);
-        *ce = S->nk - 1 - S->k_begin;
-    }
+    const int side = dk > 0 ? 0 : 1;
+    return (side == 0 ? S->slab > 0 : S->slab < S->nslabs - 1) ? side : -1;
+}
+int slab_down_side(const SlabSession *S, int dk)
+{
+    const int side = dk > 0 ? 1 : 0;
+    return (side == 0 ? S->slab > 0 : S->slab < S->nslabs - 1) ? side : -1;
 }
 
 // Enqueue the whole pipeline for this slab on S->stream (inputs/outputs on S->device).
-int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz, uint64_t nvert,
-                 const float origin[3], float dx, int band, int layout, float *d_out, Err &err)
+// Decisions every slab of the grid takes identically (dims and environment only): the
+// neighbours must agree on who writes which inbox / flag in which order.
+bool slab_multi_on() { return getenv("SDFGEN_TILE_MULTI") == nullptr || atoi(getenv("SDFGEN_TILE_MULTI")) != 0; }
+bool slab_sparse_on(const SlabSession *S)
+{
+    return sparse_sweep_supported((uint64_t)S->ni * S->nj * S->nk, S->ni, S->nj, S->nk) &&
+           (getenv("SDFGEN_SLAB_SPARSE") == nullptr || atoi(getenv("SDFGEN_SLAB_SPARSE")) != 0);
+}
+
+// Whole grid's slab boundaries and this slab's per-sweep inboxes for the first-pass launch.
+void slab_plan(const SlabSession *S, StSlabPlan &plan, TileSlab io[8])
+{
+    plan.nslabs = S->nslabs;
+    plan.slab = S->slab;
+    plan.kb.resize(S->nslabs + 1);
+    for (int r = 0; r <= S->nslabs; ++r) plan.kb[r] = (int)((long long)r * S->nk / S->nslabs);
+    for (int q = 0; q < 8; ++q) {
+        TileSlab &sl = io[q];
+        const int dk = SWEEP_DIRS[q][2];
+        const int up = slab_up_side(S, dk), down = slab_down_side(S, dk);
+        sl.on = true;
+        slab_c_range(S, dk, &sl.cs, &sl.ce);
+        sl.in = up >= 0 ? S->cl.inbox(S->comm, q) : nullptr;
+        sl.out = down >= 0 ? S->cl.inbox(S->peer[down], q) : nullptr;
+        plan.in[q] = sl.in;
+        plan.out[q] = sl.out;
+    }
+}
+
+// Every allocation, table upload and stream synchronisation of a call (ntri triangles).  A thread
+// that drives several slabs prepares all of them before it enqueues any: a host-side wait after
+// one slab's kernels are running (they wait on neighbours) would wait for work this thread has
+// not enqueued yet -- measured as a deadlock broken only by the watchdogs.
+int slab_prepare(SlabSession *S, uint64_t ntri, Err &err)
 {
     const int ni = S->ni, nj = S->nj, nk = S->nk;
     const uint64_t plane_cells = (uint64_t)ni * nj;
     const int kc = S->k_end - S->k_begin;
+    hipStream_t st = S->stream;
+    HIPCHK(hipSetDevice(S->device));
     if (!S->soup || S->cap_soup < 3 * std::max<uint64_t>(ntri, 1)) {
         if (S->soup) HIPCHK(hipFree(S->soup));
         S->soup = nullptr;
@@ -822,7 +949,59 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
         HIPCHK(hipMalloc((void **)&S->soup, 3 * std::max<uint64_t>(ntri, 1) * sizeof(float4)));
         S->cap_soup = 3 * std::max<uint64_t>(ntri, 1);
     }
+    int ti = -1;
+    for (int dk = -1; dk <= 1; dk += 2) {
+        int cs, ce;
+        slab_c_range(S, dk, &cs, &ce);
+        if (ni >= 2 && nj >= 2 && ce > cs)
+            if (int rc = st_prepare(S->wf, st, ni, nj, cs, ce, &ti))
+                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab buffers");
+    }
+    if (ni >= 2 && nj >= 2 && nk >= 2 && slab_multi_on()) {
+        StSlabPlan plan;
+        TileSlab io[8];
+        slab_plan(S, plan, io);
+        const float o0[3] = {0.f, 0.f, 0.f};
+        if (int rc = tile_sweep_multi(S->wf, st, nullptr, nullptr, o0, 1.f, ni, nj, nk, 0, 8, SWEEP_DIRS, err.buf,
+                                      err.len, &plan, true))
+            return rc;
+    }
+    if (slab_sparse_on(S)) {
+        if (int rc = sp_reserve(S->sp, plane_cells * kc, st))
+            return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse buffers");
+        if (!S->alt_mem) {
+            HIPCHK(hipMalloc((void **)&S->alt_mem, plane_cells * kc * sizeof(u64)));
+            S->alt = S->alt_mem - plane_cells * (size_t)S->k_begin;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(st));
+    S->prepared_ntri = ntri;
+    return 0;
+}
+
+int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz, uint64_t nvert,
+                 const float origin[3], float dx, int band, int layout, float *d_out, Err &err)
+{
+    const int ni = S->ni, nj = S->nj, nk = S->nk;
+    const uint64_t plane_cells = (uint64_t)ni * nj;
+    const int kc = S->k_end - S->k_begin;
+    const bool tdbg = getenv("SDFGEN_DEBUG_TIMING") != nullptr;   // diagnostics: host time per phase
+    const auto t_start = std::chrono::steady_clock::now();
+    auto tmark = [&](const char *what) {
+        if (tdbg)
+            fprintf(stderr, "slab %d enqueue %-12s %.3f ms\n", S->slab, what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count());
+    };
+    if (S->prepared_ntri != ntri || !S->soup)
+        if (int rc = slab_prepare(S, ntri, err)) return rc;
+    tmark("prepare");
     hipStream_t st = S->stream;
+    const bool do_sweep = ni >= 2 && nj >= 2 && nk >= 2 && ntri > 0;
+    const bool multi = slab_multi_on(), sparse = slab_sparse_on(S);
+    StSlabPlan plan;
+    TileSlab io[8];
+    slab_plan(S, plan, io);
+    auto tile_io = [&](int s, TileSlab &sl) { sl = io[s % 8]; };
     Grid g{origin[0], origin[1], origin[2], dx, ni, nj, nk};
     const float init = (float)(ni + nj + nk) * dx;
     const u64 init_key = ((u64)__builtin_bit_cast(uint32_t, init) << 32) | 0xffffffffull;
@@ -830,7 +1009,8 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     HIPCHK(hipEventRecord(ev[0], st));
     HIPCHK(hipMemsetAsync(S->err_flag, 0, sizeof(int), st));
     HIPCHK(hipMemsetAsync(S->evals, 0, sizeof(unsigned long long), st));
-    if (S->wf.ctrl) HIPCHK(hipMemsetAsync(S->wf.ctrl + 1, 0, 2 * sizeof(int), st));
+    if (S->wf.ctrl) HIPCHK(hipMemsetAsync(S->wf.ctrl + 1, 0, 3 * sizeof(int), st));
+    if (S->sp.ctl) HIPCHK(hipMemsetAsync(S->sp.ctl, 0, SP_NCTL * sizeof(u64), st));
     if (ntri) {
         hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, d_tri, ntri, d_xyz, nvert,
                            S->soup, S->err_flag);
@@ -847,37 +1027,122 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[2], st));
+    tmark("band");
     S->launches = 0;
-    const bool do_sweep = ni >= 2 && nj >= 2 && nk >= 2 && ntri > 0;
+    S->sparse_sweeps = 0;
+    S->tile_multi = 0;
     {
         const char *gr = getenv("SDFGEN_TILE_GRID");   // co-resident slabs on one GPU need a cap
         S->wf.grid_override = gr ? atoi(gr) : 0;
     }
-    for (int s = 0; s < 16; ++s) {
+    S->wf.clo = plane_cells * (uint64_t)S->k_begin;
+    S->wf.chi = plane_cells * (uint64_t)S->k_end;
+    S->wf.ntri = ntri;
+    S->sp.ntri = ntri;
+    u64 *cur = S->cell;   // the state buffer holding the result so far
+    for (int s = 0; s < 8 && do_sweep; ++s) {   // first pass
         HIPCHK(hipEventRecord(ev[3 + s], st));
-        if (!do_sweep) continue;
-        const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
-        TileSlab sl;
-        sl.on = true;
-        slab_c_range(S, dk, &sl.cs, &sl.ce);
-        const int par = s & 1;
-        if (dk > 0) {
-            sl.in = S->slab > 0 ? S->inbox(0, par) : nullptr;
-            sl.out = S->peer_upper ? S->peer_upper + S->plane * (0 + par) : nullptr;
-        } else {
-            sl.in = S->slab < S->nslabs - 1 ? S->inbox(1, par) : nullptr;
-            sl.out = S->peer_lower ? S->peer_lower + S->plane * (2 + par) : nullptr;
+        if (multi) {
+            if (s == 0) {
+                if (int rc = tile_sweep_multi(S->wf, st, S->soup, cur, origin, dx, ni, nj, nk, 0, 8, SWEEP_DIRS,
+                                              err.buf, err.len, &plan))
+                    return rc;
+                ++S->launches;
+                S->tile_multi = 8;
+            }
+            continue;
         }
+        const int di = SWEEP_DIRS[s][0], dj = SWEEP_DIRS[s][1], dk = SWEEP_DIRS[s][2];
+        TileSlab sl;
+        tile_io(s, sl);
         S->wf.cur_sweep = s;
-        int rc = tile_sweep(S->wf, st, S->soup, S->cell, origin, dx, ni, nj, nk, di, dj, dk, err.buf,
-                            err.len, sl);
-        if (rc) return rc;
+        if (int rc = tile_sweep(S->wf, st, S->soup, cur, origin, dx, ni, nj, nk, di, dj, dk, err.buf, err.len, sl))
+            return rc;
         ++S->launches;
     }
+    tmark("first pass");
+    const char *nsw_env = getenv("SDFGEN_DEBUG_NSWEEPS");   // diagnostics: stop after the first pass
+    if (nsw_env && atoi(nsw_env) <= 8) {
+        for (int s = 8; s < 16; ++s) HIPCHK(hipEventRecord(ev[3 + s], st));
+    } else if (do_sweep && sparse) {
+        // second pass as Jacobi + repair per slab: the state alternates between cell and alt
+        {
+            const char *e = getenv("SDFGEN_SPARSE_WORKERS");
+            S->sp.workers = e ? atoi(e) : (nslab <= (1ull << 25) ? 64 : SP_WORKERS_DEFAULT);
+        }
+        // our boundary planes into the neighbours' parity-0 halo planes, then DONE
+        SpExportParams E;
+        memset(&E, 0, sizeof(E));
+        E.cell = cur;
+        E.plane = plane_cells;
+        E.c_first = plane_cells * (u64)S->k_begin;
+        E.c_last = plane_cells * (u64)(S->k_end - 1);
+        for (int side = 0; side < 2; ++side) {
+            const bool has = side == 0 ? S->slab > 0 : S->slab < S->nslabs - 1;
+            if (!has) continue;
+            E.nb_hS[side] = S->cl.halo(S->peer[side], 1 - side, 0);
+            E.nb_flags[side] = S->cl.flags(S->peer[side]);
+        }
+        E.epoch = ++S->sync_epoch;
+        E.arrive = S->arrive;
+        HIPCHK(hipMemsetAsync(S->arrive, 0, sizeof(unsigned), st));
+        if (!getenv("SDFGEN_DEBUG_NO_EXPORT"))   // diagnostics
+            hipLaunchKernelGGL(k_sp_slab_export, dim3(grid_for(plane_cells, 256, 256)), dim3(256), 0, st, E);
+        HIPCHK(hipGetLastError());
+        u64 *other = S->alt;
+        const char *stg_env = getenv("SDFGEN_DEBUG_SPARSE_STAGE");
+        int n_sparse = nsw_env ? std::max(0, std::min(8, atoi(nsw_env) - 8)) : 8;   // diagnostics
+        if (stg_env && atoi(stg_env) == 0) n_sparse = 0;                             // diagnostics: export only
+        for (int m = 0; m < n_sparse; ++m) {
+            const int s = 8 + m;
+            HIPCHK(hipEventRecord(ev[3 + s], st));
+            SpSlabSweep L;
+            memset(&L, 0, sizeof(L));
+            L.S = cur;
+            L.X = other;
+            L.k_lo = S->k_begin;
+            L.k_hi = S->k_end;
+            for (int side = 0; side < 2; ++side) {
+                L.hS[side] = S->cl.halo(S->comm, side, m & 1);
+                L.hX[side] = S->cl.halo(S->comm, side, (m + 1) & 1);
+                L.in_ring[side] = S->cl.ring(S->comm, side);
+                const bool has = side == 0 ? S->slab > 0 : S->slab < S->nslabs - 1;
+                if (!has) continue;
+                L.nb_hX[side] = S->cl.halo(S->peer[side], 1 - side, (m + 1) & 1);
+                L.nb_ring[side] = S->cl.ring(S->peer[side], 1 - side);
+                L.nb_flags[side] = S->cl.flags(S->peer[side]);
+            }
+            L.ring_cap = S->cl.ring_cap;
+            L.flags = S->cl.flags(S->comm);
+            L.prev_epoch = S->sync_epoch;
+            L.epoch = ++S->sync_epoch;
+            L.arrive = S->arrive;
+            if (int rc = sparse_sweep_slab(S->sp, st, S->soup, L, origin, dx, ni, nj, nk, s))
+                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse sweep setup failed");
+            S->launches += 3;
+            ++S->sparse_sweeps;
+            std::swap(cur, other);
+        }
+        for (int m = n_sparse; m < 8; ++m) HIPCHK(hipEventRecord(ev[11 + m], st));
+    } else {
+        for (int s = 8; s < 16 && do_sweep; ++s) {
+            HIPCHK(hipEventRecord(ev[3 + s], st));
+            const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
+            TileSlab sl;
+            tile_io(s, sl);
+            S->wf.cur_sweep = s;
+            if (int rc = tile_sweep(S->wf, st, S->soup, cur, origin, dx, ni, nj, nk, di, dj, dk, err.buf, err.len, sl))
+                return rc;
+            ++S->launches;
+        }
+    }
+    tmark("sweeps");
+    for (int s = 0; s < 16; ++s)   // sweeps not run (tiny grids) still need their events recorded
+        if (!do_sweep) HIPCHK(hipEventRecord(ev[3 + s], st));
     HIPCHK(hipEventRecord(ev[19], st));
     {
         const uint64_t rows = (uint64_t)nj * kc;
-        hipLaunchKernelGGL(k_sign, dim3((unsigned)((rows * 64 + 255) / 256)), dim3(256), 0, st, S->cell, S->cnt, g,
+        hipLaunchKernelGGL(k_sign, dim3(grid_for(rows * 64, 256, 65536)), dim3(256), 0, st, cur, S->cnt, g,
                            layout, d_out, S->k_begin, kc);
         HIPCHK(hipGetLastError());
     }
@@ -889,11 +1154,17 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
 {
     hipStream_t st = S->stream;
     int flag = 0, wf_err[2] = {0, 0};
-    unsigned long long evals = 0;
+    unsigned long long evals = 0, sp_ctl[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpyAsync(&flag, S->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     if (S->wf.ctrl) HIPCHK(hipMemcpyAsync(wf_err, S->wf.ctrl + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (S->sparse_sweeps && S->sp.ctl) HIPCHK(hipMemcpyAsync(sp_ctl, S->sp.ctl, sizeof(sp_ctl), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&evals, S->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    {
+        char where[32];
+        snprintf(where, sizeof(where), "GPU slab %d", S->slab);
+        if (int rc = check_oob(err, where)) return rc;
+    }
     if (prof) {
         sdfgen_hip_profile p;
         memset(&p, 0, sizeof(p));
@@ -914,9 +1185,15 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         HIPCHK(hipEventElapsedTime(&ms, ev[19], ev[20]));
         p.sign_ms = ms;
         p.sweep_launches = S->launches;
-        p.sweep_impl = 3;   // Z-slab tile wavefront
+        p.sweep_impl = S->sparse_sweeps ? 2 : 1;   // as on one GPU; `slabs` says it ran split
         p.band_evals = evals;
-        p.sparse_first = 16;
+        p.sparse_sweeps = S->sparse_sweeps;
+        p.sparse_first = S->sparse_sweeps ? 8 : 16;
+        p.sparse_rechecks = sp_ctl[SP_RUNS];
+        p.sparse_claims = sp_ctl[SP_ENQ];
+        p.tile_multi = S->tile_multi;
+        p.chain_steps = S->tile_multi ? S->wf.chain_steps : 0.0;
+        p.slabs = S->nslabs;
         *prof = p;
     }
     if (wf_err[0] & 4)
@@ -925,6 +1202,12 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
     if (wf_err[0])
         return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: sweep watchdog fired (lost tile hand-off, code %d, sweep %d)",
                        S->slab, wf_err[0], wf_err[1] - 1);
+    if (sp_ctl[SP_ERR] & 16ull)
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: a neighbour slab's second-pass handshake never came", S->slab);
+    if (sp_ctl[SP_ERR] & 8ull)
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: inbound boundary ring overflow", S->slab);
+    if (sp_ctl[SP_ERR] & 4ull) return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: Jacobi list overflow", S->slab);
+    if (sp_ctl[SP_ERR]) return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: sparse sweep watchdog fired", S->slab);
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
                              (unsigned long long)nvert);
     return 0;
@@ -968,6 +1251,8 @@ int run_zslab_local(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64
         if ((rc = sdfgen_hip_slab_connect_local(S[g].h, g > 0 ? S[g - 1].h : nullptr,
                                                 g < n - 1 ? S[g + 1].h : nullptr, err.buf, err.len)))
             return rc;
+    // all allocations and uploads first, then every slab's kernels: setting a slab up while an
+    // earlier slab's kernels already wait on it can block this thread
     for (int g = 0; g < n; ++g) {
         SlabSession *T = slab_of(S[g].h);
         HIPCHK(hipSetDevice(T->device));
@@ -980,6 +1265,12 @@ int run_zslab_local(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64
         T->cap_out = 4 * nout;
         if (ntri) HIPCHK(hipMemcpyAsync(T->tri, tri, 12 * ntri, hipMemcpyHostToDevice, T->stream));
         if (nvert) HIPCHK(hipMemcpyAsync(T->xyz, xyz, 12 * nvert, hipMemcpyHostToDevice, T->stream));
+        if ((rc = slab_prepare(T, ntri, err))) return rc;
+        HIPCHK(hipStreamSynchronize(T->stream));
+    }
+    for (int g = 0; g < n; ++g) {
+        SlabSession *T = slab_of(S[g].h);
+        HIPCHK(hipSetDevice(T->device));
         if ((rc = slab_enqueue(T, T->tri, ntri, T->xyz, nvert, origin, dx, band, layout, T->out, err))) return rc;
     }
     for (int g = 0; g < n; ++g) {   // slab results into the caller's grid
@@ -1218,7 +1509,7 @@ int sdfgen_hip_slab_export(sdfgen_hip_slab *h, void *handle, char *errbuf, size_
     static_assert(sizeof(hipIpcMemHandle_t) <= SDFGEN_HIP_IPC_HANDLE_BYTES, "IPC handle size");
     HIPCHK(hipSetDevice(h->s.device));
     hipIpcMemHandle_t m;
-    HIPCHK(hipIpcGetMemHandle(&m, h->s.inbox_mem));
+    HIPCHK(hipIpcGetMemHandle(&m, h->s.comm));
     memset(handle, 0, SDFGEN_HIP_IPC_HANDLE_BYTES);
     memcpy(handle, &m, sizeof(m));
     return 0;
@@ -1233,21 +1524,22 @@ int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *h, const void *lower, const voi
     if ((S->slab > 0) != (lower != nullptr) || (S->slab < S->nslabs - 1) != (upper != nullptr))
         return err.set(SDFGEN_HIP_EINVAL, "slab %d of %d needs exactly its existing neighbours", S->slab, S->nslabs);
     HIPCHK(hipSetDevice(S->device));
-    if (lower) {
+    const void *hs[2] = {lower, upper};
+    for (int side = 0; side < 2; ++side) {
+        if (!hs[side]) continue;
         hipIpcMemHandle_t m;
-        memcpy(&m, lower, sizeof(m));
+        memcpy(&m, hs[side], sizeof(m));
         void *p = nullptr;
         HIPCHK(hipIpcOpenMemHandle(&p, m, hipIpcMemLazyEnablePeerAccess));
-        S->peer_lower = (u64 *)p;
-        S->lower_ipc = true;
-    }
-    if (upper) {
-        hipIpcMemHandle_t m;
-        memcpy(&m, upper, sizeof(m));
-        void *p = nullptr;
-        HIPCHK(hipIpcOpenMemHandle(&p, m, hipIpcMemLazyEnablePeerAccess));
-        S->peer_upper = (u64 *)p;
-        S->upper_ipc = true;
+        S->peer[side] = (char *)p;
+        S->peer_ipc[side] = true;
+        // the mapping must cover the neighbour's whole block (same grid => same layout)
+        void *base = nullptr;
+        size_t size = 0;
+        if (hipMemGetAddressRange(&base, &size, p) == hipSuccess && base &&
+            (char *)base + size < (char *)p + S->cl.bytes)
+            return err.set(SDFGEN_HIP_ERUNTIME, "IPC mapping of slab %d's neighbour is %zu bytes, expected %zu",
+                           S->slab, size, S->cl.bytes);
     }
     return 0;
 }
@@ -1270,8 +1562,8 @@ int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *h, sdfgen_hip_slab *lower, sd
         if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HIPCHK(e);
         (void)hipGetLastError();
     }
-    S->peer_lower = lower ? lower->s.inbox_mem : nullptr;
-    S->peer_upper = upper ? upper->s.inbox_mem : nullptr;
+    S->peer[0] = lower ? lower->s.comm : nullptr;
+    S->peer[1] = upper ? upper->s.comm : nullptr;
     return 0;
 }
 
@@ -1290,6 +1582,15 @@ int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *h, const uint32_t *d_tri, uint64_t 
     std::lock_guard<std::mutex> lk(S->mu);
     HIPCHK(hipSetDevice(S->device));
     return slab_enqueue(S, d_tri, ntri, d_xyz, nvert, origin, dx, exact_band, out_layout, d_phi_slab, err);
+}
+
+int sdfgen_hip_slab_prepare(sdfgen_hip_slab *h, uint64_t ntri, char *errbuf, size_t errlen)
+{
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    std::lock_guard<std::mutex> lk(h->s.mu);
+    return slab_prepare(&h->s, ntri, err);
 }
 
 int sdfgen_hip_slab_finish(sdfgen_hip_slab *h, uint64_t nvert, sdfgen_hip_profile *prof, char *errbuf, size_t errlen)
@@ -1333,6 +1634,24 @@ int sdfgen_hip_slab_run(sdfgen_hip_slab *h, const uint32_t *tri, uint64_t ntri, 
         return rc;
     HIPCHK(hipMemcpyAsync(phi_slab, S->out, 4 * nout, hipMemcpyDeviceToHost, S->stream));
     return slab_finish(S, nvert, prof, err);
+}
+
+int sdfgen_hip_slab_debug_dump(sdfgen_hip_slab *h, int which, void *out, uint64_t max_bytes, uint64_t *n_bytes)
+{
+    if (!h || !out || !n_bytes) return SDFGEN_HIP_EINVAL;
+    SlabSession *S = &h->s;
+    if (hipSetDevice(S->device) != hipSuccess || hipStreamSynchronize(S->stream) != hipSuccess) return SDFGEN_HIP_ERUNTIME;
+    const void *src = nullptr;
+    size_t bytes = 0;
+    if (which == 0) { src = S->comm; bytes = S->cl.bytes; }
+    else if (which == 1 && S->wf.ctrl) { src = S->wf.ctrl; bytes = 16 * sizeof(int); }
+    else if (which == 2 && S->wf.mdone) { src = S->wf.mdone; bytes = S->wf.cap_mtasks * sizeof(unsigned); }
+    else if (which == 3 && S->wf.mtasks) { src = S->wf.mtasks; bytes = S->wf.cap_mtasks * sizeof(int4); }
+    else if (which == 4 && S->wf.mdeps) { src = S->wf.mdeps; bytes = S->wf.cap_mtasks * ST_MAXDEP * sizeof(int); }
+    bytes = std::min<size_t>(bytes, max_bytes);
+    *n_bytes = bytes;
+    if (bytes && hipMemcpy(out, src, bytes, hipMemcpyDeviceToHost) != hipSuccess) return SDFGEN_HIP_ERUNTIME;
+    return 0;
 }
 
 int sdfgen_hip_slab_destroy(sdfgen_hip_slab *h)

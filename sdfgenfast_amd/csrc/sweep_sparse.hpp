@@ -34,6 +34,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
 
 #include "geom.hpp"
 
@@ -45,8 +48,19 @@ namespace sdfhip {
 // on everything is reset before each sweep: the work-list counters, then the Jacobi list
 // counters of SP_JPARTS parts, one 128-byte line each (a shared line serialises the
 // atomics of the whole grid: 1.4 ms per sweep at 256^3, measured).
-enum { SP_ERR = 0, SP_ENQ = 1, SP_RUNS = 2, SP_DIAG = 4, SP_QUEUE = 8, SP_HEAD = 9,
+// Z-slab words (reset per sweep): SP_INHEAD reservations of the inbound ring, SP_INDONE inbound
+// lanes finished, SP_EXIT waves exited, SP_OUTTAIL entries this slab appended to the downstream
+// slab's inbound ring.
+enum { SP_ERR = 0, SP_ENQ = 1, SP_RUNS = 2, SP_DIAG = 4, SP_QUEUE = 8, SP_HEAD = 9, SP_INHEAD = 10, SP_INDONE = 11,
+       SP_EXIT = 12, SP_OUTTAIL = 13,
        SP_JPARTS = 64, SP_JSTRIDE = 16, SP_JLIST = 16, SP_NCTL = SP_JLIST + SP_JPARTS * SP_JSTRIDE };
+// SP_ERR bits: 1 repair watchdog, 2 ring overflow, 4 Jacobi list overflow, 8 inbound ring overflow
+// (Z-slab), 16 a neighbour slab's flag never came (Z-slab watchdog).
+// Z-slab flag words in the uncached communication block (sdfgen_hip.hip SlabSession), one 128-byte
+// line each, written by a NEIGHBOUR: SP_FL_DONE + side (its repair finished: every push it made is
+// in place), SP_FL_READY + side (it has initialised its live halo: pushes may start),
+// SP_FL_COUNT + side (entries it appended to our inbound ring).  side 0 = the lower slab, 1 = upper.
+enum { SP_FL_DONE = 0, SP_FL_READY = 2, SP_FL_COUNT = 4, SP_FL_WORDS = 6, SP_FL_STRIDE = 16 };
 constexpr unsigned long long SP_PENDING_ONE = 1ull << 32;
 constexpr unsigned long long SP_TAIL_LIMIT = 0xF0000000ull;   // appends per sweep (error beyond)
 constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
@@ -74,6 +88,23 @@ struct SpParams {
     int sweep;                         // index (0..15) of this sweep
     int seen[7];                       // per neighbour slot q: s'+1 of the last earlier sweep in which
                                        // an interior cell examined that neighbour (-1: none)
+    unsigned long long c_lo;           // first cell of this launch's range (n cells from c_lo)
+    int k_lo, k_hi;                    // planes whose cells this launch owns (whole grid: 0, nk)
+    // ---- Z-slab (SLAB kernels): the neighbour planes live in uncached halo planes
+    // indexed i + ni*j, the upstream slab's changes arrive as pushes ----
+    int k_first, k_last;               // this slab's first / last plane in the sweep's k direction
+    int up_side;                       // side of the upstream slab (0 lower, 1 upper)
+    const uint32_t *hS_up;             // upstream plane's low words before the sweep
+    uint32_t *hX_up;                   // ... live (pushed by the upstream slab)
+    uint32_t *push_down_halo;          // downstream slab's live halo of our last plane (remote; null: none)
+    uint32_t *push_down_ring;          // downstream slab's inbound ring (remote)
+    uint32_t *push_up_halo;            // upstream slab's halo of our first plane for its NEXT sweep (remote)
+    uint32_t *in_ring;                 // our inbound ring: cell + 1 of upstream cells that changed (null: none)
+    unsigned long long ring_cap;
+    unsigned long long *flags;         // our flag words (written by the neighbours)
+    unsigned long long *up_flags, *down_flags;   // the neighbours' flag words (remote; null: none)
+    unsigned long long epoch;          // this sweep's synchronisation epoch
+    unsigned long long ntri;           // triangles in the soup (bounds-checked builds)
 };
 
 __device__ __forceinline__ unsigned long long sp_ld64(const unsigned long long *p)
@@ -115,20 +146,31 @@ __device__ __forceinline__ bool sp_in(const SpParams &P, int i, int j, int k)
 // if u's label has not changed since (the sweep stamped in u's low word is <= s'), c has
 // already seen that label.  A label set in this very sweep carries this sweep's stamp,
 // so the LIVE (repair) evaluation needs no extra check.
-template <bool LIVE>
+template <bool LIVE, bool SLAB = false>
 __device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned long long *L, int i, int j, int k,
                                             size_t c, unsigned long long own, int (&lab)[7])
 {
     const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
     const long long cc = (long long)c;
     const long long nb[7] = {cc - si, cc - sj, cc - si - sj, cc - sk, cc - si - sk, cc - sj - sk, cc - si - sj - sk};
+    // Z-slab: the k-upwind plane of the slab's first plane is the upstream slab's (halo plane)
+    const bool halo = SLAB && (k - P.dk < P.k_lo || k - P.dk >= P.k_hi);
+    const long long hp = (long long)i + (long long)P.ni * j;   // plane index of (i, j)
+    const long long hnb[3] = {hp, hp - P.di, hp - (long long)P.dj * P.ni};   // q = 3 (k), 4 (i,k), 5 (j,k); 6 below
     int lcq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
         // the low word (label, stamp) only: half the bytes of the 8-byte cell (a 32-bit load of
         // a 64-bit atomically stored word sees one of its stored values' halves)
-        const uint32_t *lw = reinterpret_cast<const uint32_t *>(L + nb[q]);
-        const uint32_t w = LIVE ? sp_ld32(lw) : *lw;
+        uint32_t w;
+        if (SLAB && q >= 3 && halo) {
+            const long long hq = q == 6 ? hp - P.di - (long long)P.dj * P.ni : hnb[q - 3];
+            const uint32_t *hw = (LIVE ? P.hX_up : P.hS_up) + SDF_CHK(23, hq, 0, (size_t)P.ni * P.nj);
+            w = __hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            const uint32_t *lw = reinterpret_cast<const uint32_t *>(L + SDF_CHK(22, nb[q], P.c_lo, P.c_lo + P.n));
+            w = LIVE ? sp_ld32(lw) : *lw;
+        }
         lab[q] = lbl_of(w);
         lcq[q] = lc_of(w);
     }
@@ -150,12 +192,12 @@ __device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned lo
     return f;
 }
 
-template <bool LIVE>
+template <bool LIVE, bool SLAB = false>
 __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
                                                       int k, size_t c, unsigned long long own)
 {
     int lab[7];
-    unsigned f = sp_mask<LIVE>(P, L, i, j, k, c, own, lab);
+    unsigned f = sp_mask<LIVE, SLAB>(P, L, i, j, k, c, own, lab);
     float phi = __uint_as_float((uint32_t)(own >> 32));
     int ct = lbl_of((uint32_t)own);
     bool changed = false;
@@ -184,7 +226,8 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
             ta = (qa == q) ? lab[q] : ta;
             tb = (qb == q) ? lab[q] : tb;
         }
-        const size_t ba = 3 * (size_t)(has_a ? ta : 0), bb = 3 * (size_t)(has_b ? tb : (has_a ? ta : 0));
+        const size_t ba = 3 * SDF_CHK(26, (has_a ? ta : 0), 0, P.ntri),
+                     bb = 3 * SDF_CHK(26, (has_b ? tb : (has_a ? ta : 0)), 0, P.ntri);
         const float4 a0 = P.soup[ba], a1 = P.soup[ba + 1], a2 = P.soup[ba + 2];
         const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
         float da, db;
@@ -215,11 +258,14 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
 // Request rechecks of the downstream neighbours of (i,j,k) (the cells whose upwind set
 // contains it).  Returns the first cell this call took ownership of when `claim`, so
 // the caller can run it itself; the others are queued.
+// Only cells of planes [k_lo, k_hi) are requested (a Z-slab's own planes; for an upstream slab's
+// cell -- an inbound entry -- that is the cells of this slab's first plane).
 __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i, int j, int k, size_t c, bool claim)
 {
     const bool ii = P.di > 0 ? i + 1 <= P.ni - 1 : i - 1 >= 0;
     const bool jj = P.dj > 0 ? j + 1 <= P.nj - 1 : j - 1 >= 0;
-    const bool kk = P.dk > 0 ? k + 1 <= P.nk - 1 : k - 1 >= 0;
+    const bool kk = k + P.dk >= P.k_lo && k + P.dk < P.k_hi;
+    const bool k0 = k >= P.k_lo && k < P.k_hi;   // targets in this cell's own plane
     const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
     const long long cc = (long long)c;
     // all requests in flight at once, then one reservation for the cells to queue
@@ -230,9 +276,9 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
         // same order as the upwind list: (i), (j), (i,j), (k), (i,k), (j,k), (i,j,k)
         const int m = q + 1;
         const bool ui = m & 1, uj = m & 2, uk = m & 4;
-        const bool ok = !((ui && !ii) || (uj && !jj) || (uk && !kk));
+        const bool ok = !((ui && !ii) || (uj && !jj) || (uk && !kk) || (!uk && !k0));
         tgt[q] = ok ? (size_t)(cc + (ui ? si : 0) + (uj ? sj : 0) + (uk ? sk : 0)) : ~(size_t)0;
-        old[q] = ok ? atomicAdd(&P.req[tgt[q]], 1u) : 1u;
+        old[q] = ok ? atomicAdd(&P.req[SDF_CHK(24, tgt[q], P.c_lo, P.c_lo + P.n)], 1u) : 1u;
     }
     size_t mine = ~(size_t)0;
     unsigned nq = 0;
@@ -263,15 +309,41 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
 // cells in LDS and appends them with one atomic per ~200 cells.
 constexpr int SP_JWAVE = 256;   // LDS list entries per wave
 
+// Z-slab: a cell of the slab's last plane (in the sweep's k direction) changed its label: write
+// the new low word into the downstream slab's live halo, then -- once that store has completed --
+// append the cell to the downstream slab's inbound ring (the slot is reserved locally; the
+// downstream slab turns the entry into rechecks of its first plane).  A change on the first plane
+// goes to the upstream slab's halo for its next sweep (no recheck there: it is downstream of it).
+__device__ __forceinline__ void sp_push(const SpParams &P, int i, int j, int k, size_t c, uint32_t w)
+{
+    const size_t hp = (size_t)i + (size_t)P.ni * j;
+    SDF_CHK(27, hp, 0, (size_t)P.ni * P.nj);
+    if (k == P.k_last && P.push_down_halo) {
+        __hip_atomic_store(P.push_down_halo + hp, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long t = atomicAdd(&P.ctl[SP_OUTTAIL], 1ull);
+        if (t < P.ring_cap)
+            __hip_atomic_store(P.push_down_ring + t, (uint32_t)(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        else
+            atomicOr(&P.ctl[SP_ERR], 8ull);
+    }
+    if (k == P.k_first && P.push_up_halo)
+        __hip_atomic_store(P.push_up_halo + hp, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <bool SLAB = false>
 __device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32)
 {
     const int i = (int)(c32 % (unsigned)P.ni);
     const unsigned r = c32 / (unsigned)P.ni;
     const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
-    const unsigned long long s = P.S[c32];
-    const unsigned long long y = sp_eval<false>(P, P.S, i, j, k, c32, s);
-    P.X[c32] = y;
-    if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) sp_request_downstream(P, i, j, k, c32, false);
+    const unsigned long long s = P.S[SDF_CHK(20, c32, P.c_lo, P.c_lo + P.n)];
+    const unsigned long long y = sp_eval<false, SLAB>(P, P.S, i, j, k, c32, s);
+    P.X[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = y;
+    if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) {
+        if (SLAB) sp_push(P, i, j, k, c32, (uint32_t)y);
+        sp_request_downstream(P, i, j, k, c32, false);
+    }
 }
 
 // wave-synchronous LDS hand-over between lanes of one wave
@@ -298,6 +370,7 @@ __device__ __forceinline__ void sp_jlist_flush(const SpParams &P, unsigned part,
     sp_wave_sync();
 }
 
+template <bool SLAB>
 __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 {
     __shared__ unsigned s_list[4][SP_JWAVE];
@@ -316,7 +389,7 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
     // (si, sj, sk) with carries (two integer divisions per cell cost ~30 instructions)
     int i, j, k, si, sj, sk;
     {
-        const unsigned c0 = (unsigned)(base + first), r0 = c0 / (unsigned)P.ni;
+        const unsigned c0 = (unsigned)(P.c_lo + base + first), r0 = c0 / (unsigned)P.ni;
         i = (int)(c0 % (unsigned)P.ni);
         j = (int)(r0 % (unsigned)P.nj);
         k = (int)(r0 / (unsigned)P.nj);
@@ -326,14 +399,14 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
         sk = (int)(rs / (unsigned)P.nj);
     }
     for (unsigned long long it = first; it - lane < span; it += step) {   // wave-uniform trip count
-        const unsigned long long c = base + it;
-        const bool valid = it < span && c < P.n;
-        const unsigned c32 = (unsigned)c;   // n < 2^32 (sparse_sweep_supported)
+        const bool valid = it < span && base + it < P.n;
+        const unsigned long long c = P.c_lo + base + it;
+        const unsigned c32 = (unsigned)c;   // cells < 2^32 (sparse_sweep_supported)
         unsigned f = 0;
         if (valid) {
             const unsigned long long s = P.S[c];
             int lab[7];
-            if (sp_in(P, i, j, k)) f = sp_mask<false>(P, P.S, i, j, k, c, s, lab);
+            if (sp_in(P, i, j, k)) f = sp_mask<false, SLAB>(P, P.S, i, j, k, c, s, lab);
             if (!f) P.X[c] = s;
         }
         const unsigned long long want = __ballot(f != 0u);
@@ -355,6 +428,9 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 }
 
 // Pass 1b: the listed cells, each exactly as in place (sp_eval against S).
+// Z-slab: it pushes into the neighbours' live halos, so it runs after k_sp_slab_wait saw both
+// neighbours READY.
+template <bool SLAB>
 __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
 {
     const unsigned part = blockIdx.x % SP_JPARTS;
@@ -363,7 +439,7 @@ __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
     const unsigned *list = P.jlist + (size_t)part * P.jcap;
     for (unsigned long long x = (unsigned long long)(blockIdx.x / SP_JPARTS) * blockDim.x + threadIdx.x; x < cnt;
          x += (unsigned long long)(gridDim.x / SP_JPARTS) * blockDim.x)
-        sp_jacobi_cell(P, list[x]);
+        sp_jacobi_cell<SLAB>(P, list[x]);
 }
 
 // Pass 2: drain the recheck work list.  One lane = one worker; chains are followed
@@ -371,16 +447,53 @@ __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
 // which every lane does at most one poll or one evaluation per iteration: a lane
 // spinning on an empty slot must never hold back (SIMT reconvergence) lanes of its own
 // wave whose work would fill that slot.
+//
+// Z-slab: the lanes of workgroup 0 also drain the inbound ring (cells of the upstream slab's last
+// plane that changed label; their live halo words are already in place): each entry becomes
+// requests for this slab's first-plane cells downstream of it.  A lane's inbound part is finished
+// once the upstream slab's repair has ended (its DONE flag) and every entry it appended (its
+// COUNT) is taken; local lanes stop only after all 64 inbound lanes finished and nothing is queued
+// or running.  The last wave to leave tells the downstream slab (COUNT, then DONE) and the
+// upstream slab (DONE: our pushes into its halo for its next sweep are in place).
+template <bool SLAB>
 __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 {
     constexpr size_t NONE = ~(size_t)0;
-    unsigned long long runs = 0, claims = 0, h = 0;
+    unsigned long long runs = 0, claims = 0, h = 0, h_in = 0;
     size_t e = NONE, next = NONE;
     unsigned rq = 1;
-    bool done = false, waiting = false;
-    unsigned spins = 0;
+    bool done = false, waiting = false, in_wait = false;
+    bool in_role = SLAB && P.in_ring != nullptr && blockIdx.x == 0;   // still draining the inbound ring
+    unsigned spins = 0, in_spins = 0;
     for (;;) {
-        if (!done && e == NONE) {
+        if (SLAB && in_role && e == NONE) {
+            if (!in_wait) {
+                h_in = atomicAdd(&P.ctl[SP_INHEAD], 1ull);
+                in_wait = true;
+            }
+            const unsigned v = h_in < P.ring_cap ? __hip_atomic_load(P.in_ring + h_in, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_SYSTEM) : 0u;
+            if (v) {
+                __hip_atomic_store(P.in_ring + h_in, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                in_wait = false;
+                in_spins = 0;
+                const unsigned u = v - 1;   // an upstream cell: its downstream cells here are queued
+                const int iu = (int)(u % (unsigned)P.ni);
+                const unsigned ru = u / (unsigned)P.ni;
+                sp_request_downstream(P, iu, (int)(ru % (unsigned)P.nj), (int)(ru / (unsigned)P.nj), u, false);
+            } else if (__hip_atomic_load(P.flags + (SP_FL_DONE + P.up_side) * SP_FL_STRIDE, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) >= P.epoch &&
+                       h_in >= __hip_atomic_load(P.flags + (SP_FL_COUNT + P.up_side) * SP_FL_STRIDE,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+                in_role = false;   // DONE is written after COUNT: nothing more can come
+                sp_order();
+                atomicAdd(&P.ctl[SP_INDONE], 1ull);
+            } else if (++in_spins > SP_WATCHDOG || ((in_spins & 255u) == 255u && (sp_ld64(&P.ctl[SP_ERR]) & 16ull))) {
+                atomicOr(&P.ctl[SP_ERR], 16ull);
+                in_role = false;
+                atomicAdd(&P.ctl[SP_INDONE], 1ull);
+            }
+        } else if (!done && e == NONE) {
             if (!waiting) {
                 h = atomicAdd(&P.ctl[SP_HEAD], 1ull);
                 waiting = true;
@@ -389,13 +502,14 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             const unsigned v = sp_ld32(slot);
             if (v) {
                 sp_st32(slot, 0u);
-                e = v - 1;
+                e = SDF_CHK(28, v - 1, P.c_lo, P.c_lo + P.n);
                 next = NONE;
                 rq = 1;
                 waiting = false;
                 spins = 0;
-            } else if ((sp_ld64(&P.ctl[SP_QUEUE]) >> 32) == 0ull) {
-                done = true;   // nothing queued or running anywhere: no slot can fill any more
+            } else if ((!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= 64ull) &&
+                       (sp_ld64(&P.ctl[SP_QUEUE]) >> 32) == 0ull) {
+                done = true;   // nothing queued or running anywhere (nor to come): no slot can fill any more
             } else if (++spins > SP_WATCHDOG) {
                 atomicOr(&P.ctl[SP_ERR], 1ull);
                 done = true;
@@ -414,11 +528,11 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 e = e2;
             }
 #endif
-            const unsigned long long cur = sp_ld64(P.X + e);
+            const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, e, P.c_lo, P.c_lo + P.n));
 #ifdef SP_NOEVAL_RECHECK   // diagnostics: the work list's own cost (no evaluation, no relabel)
             const unsigned long long y = cur;
 #else
-            const unsigned long long y = sp_eval<true>(P, P.X, i, j, k, e, P.S[e]);
+            const unsigned long long y = sp_eval<true, SLAB>(P, P.X, i, j, k, e, P.S[e]);
 #endif
             ++runs;
             const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
@@ -426,6 +540,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 sp_st64(P.X + e, y);
                 if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
             }
+            if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
             // retire e's requests and ask for the downstream rechecks in one round trip
             const unsigned old = atomicSub(P.req + e, rq);
             if (relabel) {
@@ -453,6 +568,115 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
     }
     if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
     if (claims) atomicAdd(&P.ctl[SP_ENQ], claims);
+    if (SLAB) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every push of this wave has landed
+        if ((threadIdx.x & 63) == 0 && atomicAdd(&P.ctl[SP_EXIT], 1ull) == gridDim.x - 1ull) {
+            if (P.down_flags) {
+                __hip_atomic_store(P.down_flags + (SP_FL_COUNT + P.up_side) * SP_FL_STRIDE, sp_ld64(&P.ctl[SP_OUTTAIL]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(P.down_flags + (SP_FL_DONE + P.up_side) * SP_FL_STRIDE, P.epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (P.up_flags)
+                __hip_atomic_store(P.up_flags + (SP_FL_DONE + 1 - P.up_side) * SP_FL_STRIDE, P.epoch, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+// Z-slab, around each sparse sweep:
+//   k_sp_slab_wait(DONE, previous epoch)  both neighbours finished the previous sweep: their pushes
+//                                         into our halo planes are in place;
+//   k_sp_slab_halo                        the live halos start as copies of the pre-sweep ones, then
+//                                         the neighbours are told they may push (READY);
+//   k_sp_jacobi                           (no pushes)
+//   k_sp_slab_wait(READY, this epoch)     both neighbours' live halos are initialised;
+//   k_sp_jlist, k_sp_recheck              (push).
+// The waits are one-workgroup launches: a wide launch whose blocks spin could starve a neighbour
+// slab sharing the device (the one-GPU tests) of the slots it needs to make progress.
+struct SpHaloParams {
+    const uint32_t *hS[2];                     // [side] pre-sweep halo planes (ni*nj low words)
+    uint32_t *hX[2];                           // [side] live halo planes
+    unsigned long long plane;
+    unsigned long long *flags;                 // ours (written by the neighbours)
+    unsigned long long *nb_flags[2];           // the lower / upper neighbour's (null: none)
+    unsigned long long epoch;
+    int word;                                  // k_sp_slab_wait: SP_FL_DONE or SP_FL_READY
+    unsigned long long *ctl;                   // sparse control words (error bits)
+    unsigned *arrive;                          // zeroed before k_sp_slab_halo
+};
+
+__global__ void __launch_bounds__(64) k_sp_slab_wait(SpHaloParams H)
+{
+    if (threadIdx.x >= 2 || !H.nb_flags[threadIdx.x]) return;
+    const unsigned long long *f = H.flags + (H.word + threadIdx.x) * SP_FL_STRIDE;
+    for (unsigned spins = 0;; ++spins) {
+        if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= H.epoch) break;
+        // fail fast once a handshake of this call has already failed (the neighbour is not coming)
+        if (spins > SP_WATCHDOG || ((spins & 255u) == 255u && (sp_ld64(&H.ctl[SP_ERR]) & 16ull))) {
+            atomicOr(&H.ctl[SP_ERR], 16ull);
+            break;
+        }
+        if (spins < 64) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(16);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sp_slab_halo(SpHaloParams H)
+{
+    for (int side = 0; side < 2; ++side) {
+        if (!H.nb_flags[side]) continue;
+        for (unsigned long long p = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; p < H.plane;
+             p += (unsigned long long)gridDim.x * blockDim.x)
+            __hip_atomic_store(H.hX[side] + p, __hip_atomic_load(H.hS[side] + p, __ATOMIC_RELAXED,
+                                                                 __HIP_MEMORY_SCOPE_SYSTEM),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(H.arrive, 1u) == gridDim.x - 1u) {
+        // the side-s neighbour sees us from its side 1 - s
+        if (H.nb_flags[0])
+            __hip_atomic_store(H.nb_flags[0] + (SP_FL_READY + 1) * SP_FL_STRIDE, H.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (H.nb_flags[1])
+            __hip_atomic_store(H.nb_flags[1] + (SP_FL_READY + 0) * SP_FL_STRIDE, H.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// Z-slab, after the tile sweeps of the first pass: our first and last planes' low words go into
+// the neighbours' pre-sweep halo planes of the first sparse sweep (parity 0), then DONE(epoch).
+struct SpExportParams {
+    const unsigned long long *cell;            // global cell index
+    unsigned long long plane;
+    unsigned long long c_first, c_last;        // first cell of plane k_lo / k_hi - 1
+    uint32_t *nb_hS[2];                        // lower neighbour's upper halo, upper neighbour's lower halo
+    unsigned long long *nb_flags[2];
+    unsigned long long epoch;
+    unsigned *arrive;
+};
+
+__global__ void __launch_bounds__(256) k_sp_slab_export(SpExportParams E)
+{
+    for (unsigned long long p = blockIdx.x * (unsigned long long)blockDim.x + threadIdx.x; p < E.plane;
+         p += (unsigned long long)gridDim.x * blockDim.x) {
+        if (E.nb_hS[0])
+            __hip_atomic_store(E.nb_hS[0] + p, (uint32_t)E.cell[E.c_first + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (E.nb_hS[1])
+            __hip_atomic_store(E.nb_hS[1] + p, (uint32_t)E.cell[E.c_last + p], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0 && atomicAdd(E.arrive, 1u) == gridDim.x - 1u) {
+        if (E.nb_flags[0])
+            __hip_atomic_store(E.nb_flags[0] + (SP_FL_DONE + 1) * SP_FL_STRIDE, E.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        if (E.nb_flags[1])
+            __hip_atomic_store(E.nb_flags[1] + (SP_FL_DONE + 0) * SP_FL_STRIDE, E.epoch, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -460,6 +684,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 // ---------------------------------------------------------------------------
 struct SparseSweepWorkspace {
     int workers = SP_WORKERS_DEFAULT;            // repair-kernel workgroups (diagnostics may lower it)
+    unsigned long long ntri = ~0ull;             // soup size for bounds-checked builds
     unsigned long long *alt = nullptr;   // the second state buffer
     unsigned *req = nullptr, *queue = nullptr, *jlist = nullptr;
     unsigned long long *ctl = nullptr;
@@ -472,39 +697,56 @@ inline bool sparse_sweep_supported(unsigned long long n, int ni, int nj, int nk)
 }
 
 template <class T>
-inline int sp_grow(T **p, size_t *cap, size_t need, bool zero)
+inline int sp_grow(T **p, size_t *cap, size_t need, bool zero, hipStream_t st)
 {
     if (*p && *cap >= need) return 0;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
     if (hipMalloc((void **)p, need * sizeof(T)) != hipSuccess) return -5;
-    if (zero && hipMemset(*p, 0, need * sizeof(T)) != hipSuccess) return -4;
+    if (zero && hipMemsetAsync(*p, 0, need * sizeof(T), st) != hipSuccess) return -4;   // (see st_grow)
     *cap = need;
     return 0;
 }
 
-// Enqueue one sparse sweep on `st`: reads *cell, writes the other buffer, then swaps
-// the two so *cell holds the result.  Returns 0 or a negative SDFGEN_HIP_E* code.
-inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long **cell,
-                        size_t *cap_cell, const float origin[3], float dx, int ni, int nj, int nk,
-                        int sweep)
+// Workspace for sparse sweeps over n cells (allocations only: a Z-slab grows it before it
+// enqueues anything, since a later hipFree would synchronise the device mid-call).
+inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, hipStream_t st)
 {
-    const int di = SP_DIRS[sweep % 8][0], dj = SP_DIRS[sweep % 8][1], dk = SP_DIRS[sweep % 8][2];
-    const unsigned long long n = (unsigned long long)ni * nj * nk;
-    const int nw = (W.workers > 0 && W.workers <= SP_WORKERS) ? W.workers : SP_WORKERS;
     const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
-    if (sp_grow(&W.alt, &W.cap_alt, n, false)) return -5;
-    if (sp_grow(&W.req, &W.cap_req, n, true)) return -5;      // stays all-zero between sweeps
-    if (sp_grow(&W.queue, &W.cap_queue, cap, true)) return -5; // slots are reset when consumed
+    if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;
+    if (sp_grow(&W.queue, &W.cap_queue, cap, true, st)) return -5;
     if (!W.ctl) {
         if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
-        if (hipMemset(W.ctl, 0, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -4;
+        if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
+    }
+    unsigned long long blocks = (n + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    blocks = (blocks + 7) / 8 * 8;
+    const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
+    const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
+    if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
+    return 0;
+}
+
+// Shared part of a sparse sweep's setup: workspace for n cells starting at c_lo (req indexed by
+// global cell), per-sweep control reset, launch geometry and the parameter block.
+inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, const float origin[3], float dx,
+                    int ni, int nj, int nk, int sweep, unsigned long long c_lo, unsigned long long n, SpParams &P,
+                    unsigned long long &blocks)
+{
+    const int di = SP_DIRS[sweep % 8][0], dj = SP_DIRS[sweep % 8][1], dk = SP_DIRS[sweep % 8][2];
+    const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
+    if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;      // stays all-zero between sweeps
+    if (sp_grow(&W.queue, &W.cap_queue, cap, true, st)) return -5; // slots are reset when consumed
+    if (!W.ctl) {
+        if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
+        if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
     }
     // per sweep: reset the list counters; error bits and statistics accumulate over the call
     if (hipMemsetAsync(W.ctl + SP_QUEUE, 0, (SP_NCTL - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
         return -4;
-    unsigned long long blocks = (n + 255) / 256;
+    blocks = (n + 255) / 256;
     if (blocks > 16384) blocks = 16384;
     blocks = (blocks + 7) / 8 * 8;   // a multiple of the 8 XCDs (k_sp_jacobi's traversal)
     // each list part holds every cell its blocks visit (~n/64), so it never overflows; sizing
@@ -512,18 +754,17 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
     const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
-    if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false)) return -5;
-    SpParams P;
+    if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
+    memset(&P, 0, sizeof(P));
     P.soup = soup;
-    P.S = *cell;
-    P.X = W.alt;
-    P.req = W.req;
+    P.req = W.req - c_lo;
     P.queue = W.queue;
     P.jlist = W.jlist;
     P.jcap = jcap;
     P.ctl = W.ctl;
     P.cap = cap;
     P.n = n;
+    P.c_lo = c_lo;
     P.ox = origin[0];
     P.oy = origin[1];
     P.oz = origin[2];
@@ -535,6 +776,9 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     P.dj = dj;
     P.dk = dk;
     P.sweep = sweep;
+    P.k_lo = 0;
+    P.k_hi = nk;
+    P.ntri = W.ntri;
     for (int q = 0; q < 7; ++q) {
         const int m = q + 1;   // neighbour slot q lies upwind along the axes in mask m
         P.seen[q] = -1;
@@ -546,12 +790,29 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
             }
         }
     }
-    hipLaunchKernelGGL(k_sp_jacobi, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    return 0;
+}
+
+// Enqueue one sparse sweep on `st`: reads *cell, writes the other buffer, then swaps
+// the two so *cell holds the result.  Returns 0 or a negative SDFGEN_HIP_E* code.
+inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long **cell,
+                        size_t *cap_cell, const float origin[3], float dx, int ni, int nj, int nk,
+                        int sweep)
+{
+    const unsigned long long n = (unsigned long long)ni * nj * nk;
+    const int nw = (W.workers > 0 && W.workers <= SP_WORKERS) ? W.workers : SP_WORKERS;
+    if (sp_grow(&W.alt, &W.cap_alt, n, false, st)) return -5;
+    SpParams P;
+    unsigned long long blocks = 0;
+    if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, 0, n, P, blocks)) return rc;
+    P.S = *cell;
+    P.X = W.alt;
+    hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
     const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
-    hipLaunchKernelGGL(k_sp_jlist, dim3((unsigned)lblocks), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
-    hipLaunchKernelGGL(k_sp_recheck, dim3(nw), dim3(64), 0, st, P);
+    hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
     // swap the state buffers (both hold n cells)
     unsigned long long *t = *cell;
@@ -560,6 +821,82 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     *cap_cell = W.cap_alt;
     W.alt = t;
     W.cap_alt = tc;
+    return 0;
+}
+
+// One sparse sweep of a Z-slab (planes [k_lo, k_hi) of the grid).  Sides: 0 = the
+// lower neighbour (planes below k_lo), 1 = the upper one.
+struct SpSlabSweep {
+    const unsigned long long *S;       // pre-sweep state, global cell index (own planes only)
+    unsigned long long *X;             // result, global cell index
+    int k_lo, k_hi;
+    const uint32_t *hS[2];             // our pre-sweep halo planes
+    uint32_t *hX[2];                   // our live halo planes
+    uint32_t *nb_hX[2];                // the neighbour's live halo of OUR boundary plane (remote)
+    uint32_t *nb_ring[2];              // the neighbour's inbound ring fed by us (remote)
+    uint32_t *in_ring[2];              // our inbound ring fed by that neighbour
+    unsigned long long ring_cap;
+    unsigned long long *flags;         // ours
+    unsigned long long *nb_flags[2];   // the neighbours' (null: no neighbour)
+    unsigned long long prev_epoch, epoch;
+    unsigned *arrive;                  // one local word (the halo kernel's arrival counter)
+};
+
+inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, const SpSlabSweep &L,
+                             const float origin[3], float dx, int ni, int nj, int nk, int sweep)
+{
+    const unsigned long long plane = (unsigned long long)ni * nj;
+    const unsigned long long c_lo = plane * L.k_lo, n = plane * (L.k_hi - L.k_lo);
+    const int nw = (W.workers > 0 && W.workers <= SP_WORKERS) ? W.workers : SP_WORKERS;
+    SpParams P;
+    unsigned long long blocks = 0;
+    if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, c_lo, n, P, blocks)) return rc;
+    SpHaloParams H;
+    memset(&H, 0, sizeof(H));
+    for (int side = 0; side < 2; ++side) {
+        H.hS[side] = L.hS[side];
+        H.hX[side] = L.hX[side];
+        H.nb_flags[side] = L.nb_flags[side];
+    }
+    H.plane = plane;
+    H.flags = L.flags;
+    H.ctl = W.ctl;
+    H.arrive = L.arrive;
+    H.word = SP_FL_DONE;
+    H.epoch = L.prev_epoch;
+    hipLaunchKernelGGL(k_sp_slab_wait, dim3(1), dim3(64), 0, st, H);
+    if (hipMemsetAsync(L.arrive, 0, sizeof(unsigned), st) != hipSuccess) return -4;
+    H.epoch = L.epoch;
+    hipLaunchKernelGGL(k_sp_slab_halo, dim3((unsigned)std::min<unsigned long long>((plane + 255) / 256, 256)),
+                       dim3(256), 0, st, H);
+    P.S = L.S;
+    P.X = L.X;
+    P.k_lo = L.k_lo;
+    P.k_hi = L.k_hi;
+    const int up = P.dk > 0 ? 0 : 1, down = 1 - up;
+    P.up_side = up;
+    P.k_first = P.dk > 0 ? L.k_lo : L.k_hi - 1;
+    P.k_last = P.dk > 0 ? L.k_hi - 1 : L.k_lo;
+    P.hS_up = L.hS[up];
+    P.hX_up = L.hX[up];
+    P.push_down_halo = L.nb_flags[down] ? L.nb_hX[down] : nullptr;
+    P.push_down_ring = L.nb_flags[down] ? L.nb_ring[down] : nullptr;
+    P.push_up_halo = L.nb_flags[up] ? L.nb_hX[up] : nullptr;
+    P.in_ring = L.nb_flags[up] ? L.in_ring[up] : nullptr;
+    P.ring_cap = L.ring_cap;
+    P.flags = L.flags;
+    P.up_flags = L.nb_flags[up];
+    P.down_flags = L.nb_flags[down];
+    P.epoch = L.epoch;
+    const char *stg = getenv("SDFGEN_DEBUG_SPARSE_STAGE");   // diagnostics: stop after kernel n (1 halo .. 4 all)
+    const int stage = stg ? atoi(stg) : 4;
+    if (stage >= 2) hipLaunchKernelGGL(k_sp_jacobi<true>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    H.word = SP_FL_READY;
+    if (stage >= 3) hipLaunchKernelGGL(k_sp_slab_wait, dim3(1), dim3(64), 0, st, H);
+    const unsigned long long lblocks = 32 * SP_JPARTS;
+    if (stage >= 3) hipLaunchKernelGGL(k_sp_jlist<true>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
+    if (stage >= 4) hipLaunchKernelGGL(k_sp_recheck<true>, dim3(nw), dim3(64), 0, st, P);
+    if (hipGetLastError() != hipSuccess) return -4;
     return 0;
 }
 

@@ -112,12 +112,15 @@ struct StSweep {
     int di, dj, dk, sweep;
     unsigned epoch;
     int seen[7];
+    int cs, ce, nK;               // oriented c range of this launch's slab for this sweep, its tile rows
+    const unsigned long long *hc_in;   // Z-slab inbox of this sweep (null: no upstream slab)
+    unsigned long long *hc_out;        // downstream slab's inbox of this sweep (null: none)
 };
 
 struct StParams {
     const float4 *soup;           // 3 float4 per triangle (xyz; w unused)
     unsigned long long *cell;     // (phi bits << 32) | closest_tri, i-fastest
-    unsigned long long *hb;       // granules of tile-row edges:  [nJ][C][A]
+    unsigned long long *hb;       // granules of tile-row edges:  [nJ][ce - cs][A] (c - cs)
     unsigned long long *hc;       // granules of tile-column edges: [nK][B][A]
     const int2 *tasks;            // (J,K) in dequeue order
     int *queue;                   // task counter (zeroed before each launch)
@@ -136,8 +139,11 @@ struct StParams {
     // c = ce-1 is published to the downstream slab's inbox hc_out.  An inbox holds one granule
     // per cell (a, b) of the plane, a and b in [-1, A) x [-1, B): index (b+1)*(A+1) + a+1.
     int cs, ce;
+    int hbC;                      // c extent of hb rows (= ce - cs)
     const unsigned long long *hc_in;
     unsigned long long *hc_out;
+    unsigned long long clo, chi;  // cells [clo, chi) this launch may address (bounds-checked builds)
+    unsigned long long ntri;      // triangles in the soup (bounds-checked builds)
     int seen[7];   // per upwind slot q: s'+1 of the last earlier sweep in which an interior cell
                    // examined that neighbour (-1: none) -- see sweep_sparse.hpp
     // MULTI: tasks of ST_MAXSW consecutive sweeps in one launch (cross-sweep overlap)
@@ -168,6 +174,7 @@ __device__ __forceinline__ void st_fail(const StParams &P, int bit)
 {
     atomicOr(P.err, bit);
     atomicMax(P.err + 1, P.sweep + 1);
+    atomicCAS(P.err + 2, 0, (P.sweep + 1) | (bit << 8));   // the first failure: sweep + 1, its bit
     atomicMax(P.queue, P.ntasks);
 }
 
@@ -251,15 +258,15 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     const int L = tid & 63;
     unsigned long long n_evals = 0, n_cpoll = 0, n_hpoll = 0, n_cpoll_own = 0;
 
-    if (SLAB && P.hc_out) {
+    if (SLAB && !MULTI && P.hc_out) {
         // publish this slab's last plane's face cells (a = -1 or b = -1; constant during the
-        // sweep) to the downstream slab before any task runs
+        // sweep) to the downstream slab before any task runs (MULTI: per task, below)
         const int nf = P.A + 1 + P.B;
         for (int f = blockIdx.x * ST_THREADS + tid; f < nf; f += gridDim.x * ST_THREADS) {
             const int a = f <= P.A ? f - 1 : -1, b = f <= P.A ? -1 : f - (P.A + 1);
-            const uint32_t w = (uint32_t)P.cell[st_phys(P, a, b, P.ce - 1)];
-            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), st_granule(P.epoch, w),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint32_t w = (uint32_t)P.cell[SDF_CHK(1, st_phys(P, a, b, P.ce - 1), P.clo, P.chi)];
+            __hip_atomic_store(P.hc_out + SDF_CHK(9, st_inbox(P, a, b), 0, (size_t)(P.A + 1) * (P.B + 1)),
+                               st_granule(P.epoch, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
     for (;;) {
@@ -282,6 +289,14 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             P.epoch = sw.epoch;
 #pragma unroll
             for (int q = 0; q < 7; ++q) P.seen[q] = sw.seen[q];
+            if (SLAB) {
+                P.cs = sw.cs;
+                P.ce = sw.ce;
+                P.hbC = sw.ce - sw.cs;
+                P.nK = sw.nK;
+                P.hc_in = sw.hc_in;
+                P.hc_out = sw.hc_out;
+            }
             if (wave == 0) {
                 // the previous sweep's tiles under and around this one: their cell stores first
                 const int dep = L < ST_MAXDEP ? P0.deps[(size_t)task * ST_MAXDEP + L] : -1;
@@ -301,6 +316,22 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             __syncthreads();
+            if (SLAB && P.hc_out && K == P.nK - 1) {
+                // The tile on the slab's last plane publishes that plane's face cells it covers
+                // (a = -1 for its b range; tile J = 0 also the b = -1 row): constant during this
+                // sweep and final for the previous one, since its dependencies above include every
+                // previous-sweep tile writing them.  (With overlapped sweeps the kernel-start
+                // publish of the per-sweep launches would race the previous sweep.)
+                const int b_lo = J * ST_T, b_hi = min(P.B, b_lo + ST_T);
+                const int nf = (b_hi - b_lo) + (J == 0 ? P.A + 1 : 0);
+                for (int f = tid; f < nf; f += ST_THREADS) {
+                    const int a = f < b_hi - b_lo ? -1 : f - (b_hi - b_lo) - 1;
+                    const int b = f < b_hi - b_lo ? b_lo + f : -1;
+                    const uint32_t w = (uint32_t)P.cell[SDF_CHK(2, st_phys(P, a, b, P.ce - 1), P.clo, P.chi)];
+                    __hip_atomic_store(P.hc_out + SDF_CHK(9, st_inbox(P, a, b), 0, (size_t)(P.A + 1) * (P.B + 1)),
+                                       st_granule(P.epoch, w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
         } else {
             const int2 JK = P.tasks[task];
             J = JK.x;
@@ -318,7 +349,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 const int b = b0 + bl, c = c0 + cl;
                 float4 v0, v1, v2;
                 uint32_t w = 0xffffffffu;
-                if (b < P.B && c < P.ce) w = (uint32_t)P.cell[st_phys(P, -1, b, c)];
+                if (b < P.B && c < P.ce) w = (uint32_t)P.cell[SDF_CHK(3, st_phys(P, -1, b, c), P.clo, P.chi)];
                 st_load_tri(P.soup, lbl_of(w), v0, v1, v2);
                 const int e = ST_RING0 + (ST_RR - 1) * ST_NCOL + cl * ST_T + bl;
                 s_ent[3 * e] = make_float4(v0.x, v0.y, v0.z, __uint_as_float(w));
@@ -340,8 +371,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             float4 v0, v1, v2;
             uint32_t w = 0xffffffffu;
             if (valid) {
-                if (inbox && L >= ST_T) w = st_inbox_word(P, P.hc_in + st_inbox(P, -1, hb_));
-                else w = (uint32_t)P.cell[st_phys(P, -1, hb_, hc_)];
+                if (inbox && L >= ST_T)
+                    w = st_inbox_word(P, P.hc_in + SDF_CHK(8, st_inbox(P, -1, hb_), 0, (size_t)(P.A + 1) * (P.B + 1)));
+                else w = (uint32_t)P.cell[SDF_CHK(4, st_phys(P, -1, hb_, hc_), P.clo, P.chi)];
             }
             st_load_tri(P.soup, lbl_of(w), v0, v1, v2);
             const int e = ST_HALO0 + L * ST_RH + (ST_RH - 1);
@@ -568,10 +600,12 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
                     s_ent[3 * slot + 1] = w1;
                     s_ent[3 * slot + 2] = w2;
-                    if (win >= 0) P.cell[st_phys(P, a, b, c)] = ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
+                    if (win >= 0)
+                        P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
+                            ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
                     const unsigned long long gran = st_granule(P.epoch, w_new);
                     if (bl == ST_T - 1 && J < P.nJ - 1)
-                        __hip_atomic_store(P.hb + ((size_t)J * P.C + c) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                        __hip_atomic_store(P.hb + ((size_t)J * P.hbC + (c - P.cs)) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
                     if (cl == ST_T - 1 && K < P.nK - 1)
                         __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
                     if (SLAB && P.hc_out && c == P.ce - 1)
@@ -608,7 +642,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             if (hlane) {
                 if (L < ST_T) {
                     hbs = b0 - 1; hcs = c0 + L; hoff = L; hvalid = hcs < P.ce; hbound = (J == 0);
-                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
+                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.hbC + (hcs - P.cs)) * P.A;
                 } else if (L < 2 * ST_T) {
                     hbs = b0 + (L - ST_T); hcs = c0 - 1; hoff = L - ST_T; hvalid = hbs < P.B;
                     hbound = (K == 0) && !inbox;
@@ -618,7 +652,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     hbs = b0 - 1; hcs = c0 - 1; hoff = 0; hvalid = true;
                     hbound = (J == 0 || K == 0) && !inbox;
                     if (inbox) hsrc = P.hc_in + st_inbox(P, 0, hbs);
-                    else if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.C + hcs) * P.A;
+                    else if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.hbC + (hcs - P.cs)) * P.A;
                 }
             }
             if (!hvalid || hbound) hsrc = P.hb;   // any valid address: unused lanes load harmlessly
@@ -629,13 +663,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             // All loads are unconditional (invalid slots read a clamped address and are
             // ignored), so hipcc's waitcnt pass can count them and waits for the stage-2
             // gathers only, leaving the younger stage-1 loads in flight.
+            // unused load slots read this lane's own column start (spread, cached), never one hot
+            // address; lanes off the tile's edge read the tile's first column (a Z-slab holds only
+            // its own planes: (0, 0, 0) may lie in another GPU's slab).  (b0, c0: the tile's corner,
+            // before the batch registers below shadow the name c0.)
+            const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, b0, c0);
             int fA = 0, gA = 0;                    // own steps [fA, fA+gA) whose cells are in c0..c3
             int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
             unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
             static_assert(ST_G == 4 || ST_G == 2, "helper pipeline is written out for 2- or 4-element batches");
-            // unused load slots read this lane's own column start (spread, cached), never one hot address
-            const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, 0, 0);
             unsigned idle = 0;
             for (;;) {
                 // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
@@ -682,9 +719,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
 #define ST_GATHER(g, cg, qg)                                                                          \
-    const size_t so##g = 3 * (size_t)(ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : 0); \
+    const size_t so##g = 3 * SDF_CHK(11, (ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : 0), 0, P.ntri); \
     const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
-    const size_t sh##g = 3 * (size_t)((g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : 0); \
+    const size_t sh##g = 3 * SDF_CHK(12, ((g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : 0), 0, P.ntri); \
     const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
                 ST_GATHER(0, c0, q0)
                 ST_GATHER(1, c1, q1)
@@ -707,9 +744,10 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
         const size_t ix_ = ok_ ? st_phys(P, a_, b, c) : dummy;                                         \
-        cn = P.cell[ix_];                                                                              \
+        cn = P.cell[SDF_CHK(6, ix_, P.clo, P.chi)];                                                    \
         const unsigned long long *src_ =                                                               \
-            (g) >= hcB ? P.cell + dummy : (hbound ? P.cell + st_phys(P, hB + (g), hbs, hcs) : hsrc + hB + (g)); \
+            (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
+                       : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + hB + (g)); \
         qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE);                                        \
     }
                 // Always issued (a fixed count keeps the waits below precise); slots with nothing
@@ -800,6 +838,7 @@ struct TileSweepWorkspace {
     int grid_override = 0;     // diagnostics: cap on resident workgroups
     int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
     bool skip_seen = true;     // the "already examined" skip (diagnostics can turn it off)
+    unsigned long long clo = 0, chi = ~0ull, ntri = ~0ull;   // address bounds for bounds-checked builds
     size_t cap_hb = 0, cap_hc = 0;
     // task tables (dequeue order) for up to two tile grids: a Z-slab alternates between
     // two c extents (k-up and k-down sweeps), and a table must not be rewritten while a
@@ -819,12 +858,17 @@ struct TileSweepWorkspace {
     unsigned *mdone = nullptr;
     size_t cap_mtasks = 0;
     long long mkey = -1;   // (ni, nj, nk, first sweep, count) of the uploaded graph
+    double chain_steps = 0.0;   // modelled critical path of that graph, in steps
     unsigned mepoch = 0;
 };
 
 inline bool tile_sweep_supported(int ni, int nj, int nk) { return ni >= 2 && nj >= 2 && nk >= 2; }
 
-inline int st_grow(unsigned long long **p, size_t *cap, size_t need)
+// Memsets and uploads of these helpers go on the caller's stream (then, where the host data
+// dies, a sync of THAT stream): a synchronous hipMemset/hipMemcpy was measured to block until
+// other streams' kernels finished -- with Z-slabs driven from one thread those kernels wait on
+// the very slab being set up.
+inline int st_grow(unsigned long long **p, size_t *cap, size_t need, hipStream_t st)
 {
     if (*p && *cap >= need) return 0;
     if (*p) (void)hipFree(*p);
@@ -832,7 +876,7 @@ inline int st_grow(unsigned long long **p, size_t *cap, size_t need)
     *cap = 0;
     if (hipMalloc((void **)p, need * sizeof(unsigned long long)) != hipSuccess) return -5;
     // tags are epochs >= 1: zeroed granules can never look published
-    if (hipMemset(*p, 0, need * sizeof(unsigned long long)) != hipSuccess) return -4;
+    if (hipMemsetAsync(*p, 0, need * sizeof(unsigned long long), st) != hipSuccess) return -4;
     *cap = need;
     return 0;
 }
@@ -845,27 +889,22 @@ struct TileSlab {
     unsigned long long *out = nullptr;        // downstream slab's inbox for plane ce-1 (null: last)
 };
 
-// Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
-inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
-                      const float origin[3], float dx, int ni, int nj, int nk, int di, int dj,
-                      int dk, char *err, size_t errlen, const TileSlab &slab = TileSlab())
+// Buffers and the task table of one sweep over oriented c in [cs, ce).  Growing a buffer or
+// replacing a task table synchronises the stream (a running launch may still use the old one).
+// *ti: the task table slot.  Returns 0 or a negative SDFGEN_HIP_E* code.
+inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int cs, int ce, int *ti_out)
 {
-    const int A = ni - 1, B = nj - 1, C = nk - 1;
-    const int cs = slab.on ? slab.cs : 0, ce = slab.on ? slab.ce : C;
+    const int A = ni - 1, B = nj - 1;
     const int nJ = (B + ST_T - 1) / ST_T, nK = (ce - cs + ST_T - 1) / ST_T;
     const int ntasks = nJ * nK;
-    auto fail = [&](int code, const char *msg) {
-        if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
-        return code;
-    };
-    // buffers only grow; replacing one while an earlier launch may still use it needs a sync
-    if (W.cap_hb < (size_t)nJ * C * A || W.cap_hc < (size_t)nK * B * A) (void)hipStreamSynchronize(st);
-    if (st_grow(&W.hb, &W.cap_hb, (size_t)nJ * C * A)) return fail(-5, "halo buffer allocation failed");
-    if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A)) return fail(-5, "halo buffer allocation failed");
+    const size_t nhb = (size_t)nJ * (ce - cs) * A;
+    if (W.cap_hb < nhb || W.cap_hc < (size_t)nK * B * A) (void)hipStreamSynchronize(st);
+    if (st_grow(&W.hb, &W.cap_hb, nhb, st)) return -5;
+    if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A, st)) return -5;
     if (!W.ctrl) {
-        if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
-        if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
-        if (hipMemset(W.ctrl, 0, 16 * sizeof(int)) != hipSuccess) return fail(-4, "memset");
+        if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return -5;
+        if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return -5;
+        if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return -4;
     }
     int ti = (W.task_nJ[0] == nJ && W.task_nK[0] == nK) ? 0 : (W.task_nJ[1] == nJ && W.task_nK[1] == nK) ? 1 : -1;
     if (ti < 0) {
@@ -883,15 +922,34 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
             if (W.tasks[ti]) (void)hipFree(W.tasks[ti]);
             W.tasks[ti] = nullptr;
             W.cap_tasks[ti] = 0;
-            if (hipMalloc((void **)&W.tasks[ti], std::max(ntasks, 1) * sizeof(int2)) != hipSuccess)
-                return fail(-5, "task table");
+            if (hipMalloc((void **)&W.tasks[ti], std::max(ntasks, 1) * sizeof(int2)) != hipSuccess) return -5;
             W.cap_tasks[ti] = std::max(ntasks, 1);
         }
-        if (ntasks && hipMemcpy(W.tasks[ti], t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess)
-            return fail(-4, "task table upload");
+        if (ntasks && (hipMemcpyAsync(W.tasks[ti], t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice, st) != hipSuccess ||
+                       hipStreamSynchronize(st) != hipSuccess))
+            return -4;
         W.task_nJ[ti] = nJ;
         W.task_nK[ti] = nK;
     }
+    *ti_out = ti;
+    return 0;
+}
+
+// Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
+inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
+                      const float origin[3], float dx, int ni, int nj, int nk, int di, int dj,
+                      int dk, char *err, size_t errlen, const TileSlab &slab = TileSlab())
+{
+    const int A = ni - 1, B = nj - 1, C = nk - 1;
+    const int cs = slab.on ? slab.cs : 0, ce = slab.on ? slab.ce : C;
+    const int nJ = (B + ST_T - 1) / ST_T, nK = (ce - cs + ST_T - 1) / ST_T;
+    const int ntasks = nJ * nK;
+    auto fail = [&](int code, const char *msg) {
+        if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
+        return code;
+    };
+    int ti = -1;
+    if (int rc = st_prepare(W, st, ni, nj, cs, ce, &ti)) return fail(rc, "buffer or task table allocation failed");
     if (++W.epoch == 0) ++W.epoch;   // 0 = never published
     if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     StParams P;
@@ -905,7 +963,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.stats = W.count ? W.stats : nullptr;
     P.trace = nullptr;
     if (W.trace_sweep >= 0 && W.trace_sweep == W.cur_sweep) {
-        if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks)) return fail(-5, "trace");
+        if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(-5, "trace");
         P.trace = W.trace;
     }
     P.ox = origin[0];
@@ -940,8 +998,12 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
         }
     }
     P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
+    P.clo = W.clo;
+    P.chi = W.chi;
+    P.ntri = W.ntri;
     P.cs = cs;
     P.ce = ce;
+    P.hbC = ce - cs;
     P.hc_in = slab.on ? slab.in : nullptr;
     P.hc_out = slab.on ? slab.out : nullptr;
     if (ntasks <= 0) return 0;
@@ -962,96 +1024,198 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     return 0;
 }
 
-// Physical (j or k) index range of oriented tile T along an axis of n cells swept in direction d.
-inline void st_tile_range(int T, int n, int d, int *lo, int *hi)
+// Oriented c range [cs, ce) of Z-slab [kb, ke) of an nk-plane grid for a sweep with k direction dk:
+// the slab's own planes, c = k - 1 (dk > 0) or nk - 2 - k (dk < 0); DESIGN.md §7.
+inline void st_slab_c_range(int kb, int ke, int nk, int dk, int *cs, int *ce)
 {
-    const int bl = ST_T * T, bh = std::min(ST_T * T + ST_T - 1, n - 2);   // oriented b in [0, n-1)
-    if (d > 0) { *lo = bl + 1; *hi = bh + 1; }
-    else { *lo = n - 2 - bh; *hi = n - 2 - bl; }
+    if (dk > 0) {
+        *cs = std::max(kb, 1) - 1;
+        *ce = ke - 1;
+    } else {
+        *cs = nk - 1 - std::min(ke, nk - 1);
+        *ce = nk - 1 - kb;
+    }
 }
+
+// Physical index range [lo, hi] of oriented tile T (edge ST_T) over oriented [c0, c1) of an axis of
+// n cells swept in direction d (oriented x = p - 1 for d > 0, n - 2 - p for d < 0).
+inline void st_tile_phys(int T, int c0, int c1, int n, int d, int *lo, int *hi)
+{
+    const int xl = c0 + ST_T * T, xh = std::min(c0 + ST_T * T + ST_T, c1) - 1;
+    if (d > 0) { *lo = xl + 1; *hi = xh + 1; }
+    else { *lo = n - 2 - xh; *hi = n - 2 - xl; }
+}
+
+// Tiles [*t0, *t1] of the oriented range [c0, c1) (direction d) that cover any physical index in
+// [lo, hi]; false if none.
+inline bool st_tiles_covering(int lo, int hi, int c0, int c1, int n, int d, int *t0, int *t1)
+{
+    int xl, xh;   // oriented image of [lo, hi]
+    if (d > 0) { xl = lo - 1; xh = hi - 1; }
+    else { xl = n - 2 - hi; xh = n - 2 - lo; }
+    xl = std::max(xl, c0);
+    xh = std::min(xh, c1 - 1);
+    if (xl > xh) return false;
+    *t0 = (xl - c0) / ST_T;
+    *t1 = (xh - c0) / ST_T;
+    return true;
+}
+
+// Z-slab plan of a multi-sweep launch: the slab boundaries of the whole grid (so every slab
+// derives the same global schedule), this launch's slab and its per-sweep inboxes.
+struct StSlabPlan {
+    int nslabs = 1, slab = 0;
+    std::vector<int> kb;                               // nslabs + 1 plane boundaries
+    const unsigned long long *in[ST_MAXSW] = {};       // per sweep: this slab's inbox (null: no upstream)
+    unsigned long long *out[ST_MAXSW] = {};            // per sweep: the downstream slab's inbox (null: none)
+};
 
 // Sweeps s0 .. s0+ns-1 (first pass) in ONE persistent launch: the tasks of all of them in a
 // topological order by an estimated start time, so a sweep's first tiles start while the
 // previous sweep's last tiles still run.  Each task waits for the tiles of
 // the previous sweep that cover its columns (one cell of margin on every side: the face
 // cells it reads and the cells a neighbour tile of the previous sweep reads).
+// Z-slabs (plan.nslabs > 1): the schedule is computed for the tiles of ALL slabs -- a tile on a
+// slab's first plane follows the upstream slab's tile on its last plane like any upstream tile --
+// and this launch runs its own slab's tasks in that global order.  Every wait of a task (its
+// previous-sweep tiles in this slab, the upstream slab's granules of this sweep) is on a task
+// earlier in the global order, so the globally earliest unfinished task can always be claimed
+// and run: no cross-GPU deadlock whatever the residency.
 inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
                             const float origin[3], float dx, int ni, int nj, int nk, int s0, int ns,
-                            const int (*dirs)[3], char *err, size_t errlen)
+                            const int (*dirs)[3], char *err, size_t errlen, const StSlabPlan *plan = nullptr,
+                            bool prepare_only = false)
 {
     const int A = ni - 1, B = nj - 1, C = nk - 1;
-    const int nJ = (B + ST_T - 1) / ST_T, nK = (C + ST_T - 1) / ST_T;
-    const int per = nJ * nK, ntasks = ns * per;
+    const int nJ = (B + ST_T - 1) / ST_T;
     auto fail = [&](int code, const char *msg) {
         if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
         return code;
     };
-    if (ns < 1 || ns > ST_MAXSW || per <= 0) return fail(-1, "bad multi-sweep request");
-    const size_t nhb = (size_t)nJ * C * A, nhc = (size_t)nK * B * A;
+    StSlabPlan one;
+    if (!plan) {
+        one.kb = {0, nk};
+        plan = &one;
+    }
+    const int nsl = plan->nslabs, me = plan->slab;
+    if (ns < 1 || ns > ST_MAXSW || nJ <= 0 || (int)plan->kb.size() != nsl + 1) return fail(-1, "bad multi-sweep request");
+    // per (sweep q, slab r): oriented c range and tile rows
+    std::vector<int> cs((size_t)ns * nsl), ce((size_t)ns * nsl), nKq((size_t)ns * nsl);
+    for (int q = 0; q < ns; ++q)
+        for (int r = 0; r < nsl; ++r) {
+            const size_t x = (size_t)q * nsl + r;
+            st_slab_c_range(plan->kb[r], plan->kb[r + 1], nk, dirs[(s0 + q) % 8][2], &cs[x], &ce[x]);
+            nKq[x] = std::max(0, (ce[x] - cs[x] + ST_T - 1) / ST_T);
+        }
+    // this slab's halo buffers: hb [nJ][ce - cs][A], hc [nK][B][A] per sweep
+    size_t nhb = 0, nhc = 0;
+    for (int q = 0; q < ns; ++q) {
+        const size_t x = (size_t)q * nsl + me;
+        nhb = std::max(nhb, (size_t)nJ * (size_t)std::max(ce[x] - cs[x], 0) * A);
+        nhc = std::max(nhc, (size_t)nKq[x] * B * A);
+    }
+    nhb = std::max<size_t>(nhb, 1);
+    nhc = std::max<size_t>(nhc, 1);
     if (W.cap_mhb < ns * nhb || W.cap_mhc < ns * nhc) (void)hipStreamSynchronize(st);
-    if (st_grow(&W.mhb, &W.cap_mhb, ns * nhb)) return fail(-5, "halo buffer allocation failed");
-    if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc)) return fail(-5, "halo buffer allocation failed");
+    if (st_grow(&W.mhb, &W.cap_mhb, ns * nhb, st)) return fail(-5, "halo buffer allocation failed");
+    if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc, st)) return fail(-5, "halo buffer allocation failed");
     if (!W.ctrl) {
         if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
         if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
-        if (hipMemset(W.ctrl, 0, 16 * sizeof(int)) != hipSuccess) return fail(-4, "memset");
+        if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     }
+    int ntasks = 0;
+    for (int q = 0; q < ns; ++q) ntasks += nJ * nKq[(size_t)q * nsl + me];
     long long key = ((((long long)ni * 65536 + nj) * 65536 + nk) * 64 + s0) * 16 + ns;
+    key = key * 131 + nsl * 17 + me;
     if (const char *e = getenv("SDFGEN_TILE_WC")) key ^= (long long)(atof(e) * 1000.0) << 50;
     if (W.mkey != key) {
         (void)hipStreamSynchronize(st);   // the tables may still be read by a running launch
-        // ranges of every tile of every sweep, then estimated starts (in units of one tile hop
-        // = ST_T steps): +1 per upstream tile of the same sweep, + the tile duration after
-        // each previous-sweep tile it waits for
+        // Global tile ids: sweep q, slab r, tile (J, K).  Estimated starts (in units of one tile
+        // hop = ST_T steps): +1 per upstream tile of the same sweep (across slab boundaries too),
+        // + the tile duration after each previous-sweep tile of the same slab it waits for.
         double wc = (A + 2.0 * (ST_T - 1)) / ST_T;
         if (const char *e = getenv("SDFGEN_TILE_WC")) wc *= atof(e);   // diagnostics: schedule model
         if (!(wc > 0.0)) wc = 1.0;
-        std::vector<double> key_est((size_t)ntasks, 0.0);
-        std::vector<std::vector<int>> dep((size_t)ntasks);
-        auto id = [&](int q, int J, int K) { return (q * nJ + J) * nK + K; };
+        std::vector<size_t> base((size_t)ns * nsl + 1, 0);
+        for (size_t x = 0; x < (size_t)ns * nsl; ++x) base[x + 1] = base[x] + (size_t)nJ * nKq[x];
+        const size_t nall = base[(size_t)ns * nsl];
+        auto gid = [&](int q, int r, int J, int K) { return base[(size_t)q * nsl + r] + (size_t)J * nKq[(size_t)q * nsl + r] + K; };
+        std::vector<double> kv(nall, 0.0);
+        std::vector<std::vector<int>> dep;   // this slab's tasks only: global ids of awaited tiles
+        std::vector<size_t> mine;            // global ids of this slab's tasks
         for (int q = 0; q < ns; ++q) {
             const int *d = dirs[(s0 + q) % 8], *dp = dirs[(s0 + q + 7) % 8];
-            for (int J = 0; J < nJ; ++J)
-                for (int K = 0; K < nK; ++K) {
-                    double kv = 0.0;
-                    if (J) kv = std::max(kv, key_est[id(q, J - 1, K)] + 1.0);
-                    if (K) kv = std::max(kv, key_est[id(q, J, K - 1)] + 1.0);
-                    if (q) {
-                        int jl, jh, kl, kh;
-                        st_tile_range(J, nj, d[1], &jl, &jh);
-                        st_tile_range(K, nk, d[2], &kl, &kh);
-                        --jl; ++jh; --kl; ++kh;
-                        for (int J2 = 0; J2 < nJ; ++J2) {
-                            int a0, a1;
-                            st_tile_range(J2, nj, dp[1], &a0, &a1);
-                            if (a1 < jl || a0 > jh) continue;
-                            for (int K2 = 0; K2 < nK; ++K2) {
-                                int c0, c1;
-                                st_tile_range(K2, nk, dp[2], &c0, &c1);
-                                if (c1 < kl || c0 > kh) continue;
-                                dep[id(q, J, K)].push_back(id(q - 1, J2, K2));
-                                kv = std::max(kv, key_est[id(q - 1, J2, K2)] + wc);
-                            }
+            // slabs in flow order: the k-up sweep enters at slab 0, the k-down sweep at the last
+            for (int rr = 0; rr < nsl; ++rr) {
+                const int r = d[2] > 0 ? rr : nsl - 1 - rr;
+                const int ru = d[2] > 0 ? r - 1 : r + 1;   // upstream slab of this sweep
+                const size_t x = (size_t)q * nsl + r;
+                for (int J = 0; J < nJ; ++J)
+                    for (int K = 0; K < nKq[x]; ++K) {
+                        double v = 0.0;
+                        if (J) v = std::max(v, kv[gid(q, r, J - 1, K)] + 1.0);
+                        if (K) v = std::max(v, kv[gid(q, r, J, K - 1)] + 1.0);
+                        else if (ru >= 0 && ru < nsl && nKq[(size_t)q * nsl + ru] > 0)
+                            v = std::max(v, kv[gid(q, ru, J, nKq[(size_t)q * nsl + ru] - 1)] + 1.0);
+                        std::vector<int> dj;
+                        if (q) {
+                            const size_t xp = (size_t)(q - 1) * nsl + r;
+                            int jl, jh, kl, kh;
+                            st_tile_phys(J, 0, B, nj, d[1], &jl, &jh);
+                            st_tile_phys(K, cs[x], ce[x], nk, d[2], &kl, &kh);
+                            int J0, J1, K0, K1;
+                            if (st_tiles_covering(jl - 1, jh + 1, 0, B, nj, dp[1], &J0, &J1) &&
+                                st_tiles_covering(kl - 1, kh + 1, cs[xp], ce[xp], nk, dp[2], &K0, &K1))
+                                for (int J2 = J0; J2 <= J1; ++J2)
+                                    for (int K2 = K0; K2 <= K1; ++K2) {
+                                        const size_t u = gid(q - 1, r, J2, K2);
+                                        v = std::max(v, kv[u] + wc);
+                                        if (r == me) dj.push_back((int)u);
+                                    }
                         }
-                        if (dep[id(q, J, K)].size() > (size_t)ST_MAXDEP) return fail(-1, "tile dependency overflow");
+                        kv[gid(q, r, J, K)] = v;
+                        if (r == me) {
+                            if (dj.size() > (size_t)ST_MAXDEP) return fail(-1, "tile dependency overflow");
+                            mine.push_back(gid(q, r, J, K));
+                            dep.push_back(std::move(dj));
+                        }
                     }
-                    key_est[id(q, J, K)] = kv;
-                }
+            }
         }
+        if ((int)mine.size() != ntasks) return fail(-1, "task count mismatch");
+        // modelled critical path of the launch (all slabs), in compute steps: the latency
+        // roofline's chain length (bench.py roofline.latency)
+        double kmax = 0.0;
+        for (double x : kv) kmax = std::max(kmax, x);
+        W.chain_steps = (kmax + wc) * ST_T;
+        // this slab's tasks by estimated start (ties: global id), then local positions of the deps
         std::vector<int> order((size_t)ntasks);
         for (int t = 0; t < ntasks; ++t) order[t] = t;
-        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return key_est[x] < key_est[y]; });
-        std::vector<int> pos((size_t)ntasks);
-        for (int r = 0; r < ntasks; ++r) pos[order[r]] = r;
+        std::stable_sort(order.begin(), order.end(), [&](int x, int y) { return kv[mine[x]] < kv[mine[y]]; });
+        std::vector<int> pos_of_gid_local;   // global id -> local position (this slab's tasks)
+        std::vector<std::pair<size_t, int>> gpos((size_t)ntasks);
+        for (int rnk = 0; rnk < ntasks; ++rnk) gpos[rnk] = std::make_pair(mine[order[rnk]], rnk);
+        std::sort(gpos.begin(), gpos.end());
+        auto local_pos = [&](size_t g) {
+            auto it = std::lower_bound(gpos.begin(), gpos.end(), std::make_pair(g, -1));
+            return (it != gpos.end() && it->first == g) ? it->second : -1;
+        };
         std::vector<int4> mt((size_t)ntasks);
         std::vector<int> md((size_t)ntasks * ST_MAXDEP, -1);
-        for (int r = 0; r < ntasks; ++r) {
-            const int t = order[r], q = t / per, J = (t % per) / nK, K = t % nK;
-            mt[r] = make_int4(J, K, q, 0);
+        for (int rnk = 0; rnk < ntasks; ++rnk) {
+            const int t = order[rnk];
+            const size_t g = mine[t];
+            int q = 0;
+            while (g >= base[(size_t)(q + 1) * nsl]) ++q;
+            const size_t x = (size_t)q * nsl + me;
+            const int J = (int)((g - base[x]) / nKq[x]), K = (int)((g - base[x]) % nKq[x]);
+            mt[rnk] = make_int4(J, K, q, 0);
             int m = 0;
             for (int u : dep[t]) {
-                if (pos[u] >= r) return fail(-1, "tile order not topological");
-                md[(size_t)r * ST_MAXDEP + m++] = pos[u];
+                const int pu = local_pos((size_t)u);
+                if (pu < 0 || pu >= rnk) return fail(-1, "tile order not topological");
+                md[(size_t)rnk * ST_MAXDEP + m++] = pu;
             }
         }
         if (W.cap_mtasks < (size_t)ntasks) {
@@ -1062,18 +1226,21 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
             W.mdeps = nullptr;
             W.mdone = nullptr;
             W.cap_mtasks = 0;
-            if (hipMalloc((void **)&W.mtasks, ntasks * sizeof(int4)) != hipSuccess ||
-                hipMalloc((void **)&W.mdeps, (size_t)ntasks * ST_MAXDEP * sizeof(int)) != hipSuccess ||
-                hipMalloc((void **)&W.mdone, ntasks * sizeof(unsigned)) != hipSuccess)
+            if (hipMalloc((void **)&W.mtasks, std::max(ntasks, 1) * sizeof(int4)) != hipSuccess ||
+                hipMalloc((void **)&W.mdeps, (size_t)std::max(ntasks, 1) * ST_MAXDEP * sizeof(int)) != hipSuccess ||
+                hipMalloc((void **)&W.mdone, std::max(ntasks, 1) * sizeof(unsigned)) != hipSuccess)
                 return fail(-5, "task graph allocation failed");
-            if (hipMemset(W.mdone, 0, ntasks * sizeof(unsigned)) != hipSuccess) return fail(-4, "memset");
-            W.cap_mtasks = ntasks;
+            if (hipMemsetAsync(W.mdone, 0, std::max(ntasks, 1) * sizeof(unsigned), st) != hipSuccess)
+                return fail(-4, "memset");
+            W.cap_mtasks = std::max(ntasks, 1);
         }
-        if (hipMemcpy(W.mtasks, mt.data(), ntasks * sizeof(int4), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(W.mdeps, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+        if (ntasks && (hipMemcpyAsync(W.mtasks, mt.data(), ntasks * sizeof(int4), hipMemcpyHostToDevice, st) != hipSuccess ||
+                       hipMemcpyAsync(W.mdeps, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
+                       hipStreamSynchronize(st) != hipSuccess))
             return fail(-4, "task graph upload");
         W.mkey = key;
     }
+    if (prepare_only) return 0;   // buffers and tables in place (Z-slabs: before anything is enqueued)
     if (++W.mepoch == 0) ++W.mepoch;   // completion flags of this launch (0 = never)
     if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     StParams P;
@@ -1095,17 +1262,22 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     P.B = B;
     P.C = C;
     P.nJ = nJ;
-    P.nK = nK;
+    P.nK = nKq[me];
     P.ntasks = ntasks;
     P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
-    P.cs = 0;
-    P.ce = C;
+    P.cs = cs[me];
+    P.ce = ce[me];
+    P.hbC = ce[me] - cs[me];
+    P.clo = W.clo;
+    P.chi = W.chi;
+    P.ntri = W.ntri;
     P.mtasks = W.mtasks;
     P.deps = W.mdeps;
     P.done = W.mdone;
     P.call_epoch = W.mepoch;
     for (int q = 0; q < ns; ++q) {
         const int sw = s0 + q, *d = dirs[sw % 8];
+        const size_t x = (size_t)q * nsl + me;
         StSweep &S = P.sw[q];
         S.hb = W.mhb + q * nhb;
         S.hc = W.mhc + q * nhc;
@@ -1113,8 +1285,13 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
         S.dj = d[1];
         S.dk = d[2];
         S.sweep = sw;
-        if (++W.epoch == 0) ++W.epoch;
+        if (++W.epoch == 0) ++W.epoch;   // one epoch per sweep, as tile_sweep: slabs stay in step
         S.epoch = W.epoch;
+        S.cs = cs[x];
+        S.ce = ce[x];
+        S.nK = nKq[x];
+        S.hc_in = nsl > 1 ? plan->in[q] : nullptr;
+        S.hc_out = nsl > 1 ? plan->out[q] : nullptr;
         for (int qq = 0; qq < 7; ++qq) {   // the "already examined" rule, as in tile_sweep
             const int m = qq + 1;
             S.seen[qq] = -1;
@@ -1127,9 +1304,11 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
             }
         }
     }
+    if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
-    hipLaunchKernelGGL((k_sweep_tile<false, false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    if (nsl > 1) hipLaunchKernelGGL((k_sweep_tile<true, false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    else hipLaunchKernelGGL((k_sweep_tile<false, false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }

@@ -24,7 +24,7 @@ import numpy as np
 
 from . import _lib
 
-__all__ = ["slab_range", "make_level_set3", "release"]
+__all__ = ["slab_range", "make_level_set3", "control_group", "release"]
 
 _sessions: dict = {}
 
@@ -41,14 +41,40 @@ def _dist():
     return dist
 
 
-def _control_group(dist, group):
-    """A gloo group for host-side objects when the given group is not gloo (e.g. nccl)."""
+def _group_ranks(dist, group):
+    """Global ranks of `group` in group-rank order (the default group: 0..world-1)."""
+    if group is None or group == dist.group.WORLD:
+        return list(range(dist.get_world_size()))
+    return list(dist.get_process_group_ranks(group))
+
+
+def control_group(group=None):
+    """The gloo group that carries this module's host-side objects (IPC handles, barriers,
+    the gather) for `group`: `group` itself when it is gloo.  For a non-gloo group (e.g. the
+    nccl default group) a gloo group over exactly the same ranks is created by
+    torch.distributed.new_group, which is collective over the DEFAULT group: every process
+    of the default group must take part.  That holds automatically for the default group
+    (every rank calls make_level_set3); for a non-gloo SUBGROUP call this function on every
+    rank of the default group, members or not, before the first make_level_set3 on it."""
+    dist = _dist()
     if dist.get_backend(group) == "gloo":
         return group
-    key = ("gloo", id(group))
+    ranks = _group_ranks(dist, group)
+    key = ("gloo", tuple(ranks))
     if key not in _sessions:
-        _sessions[key] = dist.new_group(backend="gloo")
+        _sessions[key] = dist.new_group(ranks=ranks, backend="gloo")
     return _sessions[key]
+
+
+def _control_group(dist, group):
+    if dist.get_backend(group) == "gloo":
+        return group
+    ranks = _group_ranks(dist, group)
+    key = ("gloo", tuple(ranks))
+    if key not in _sessions and len(ranks) != dist.get_world_size():
+        raise ValueError("make_level_set3 on a non-gloo subgroup needs its gloo control group: call "
+                         "sdfgenfast_amd.distributed.control_group(group) on EVERY rank of the default group first")
+    return control_group(group)
 
 
 def _gpu_session(dist, group, device: int, dims, world: int, rank: int):
@@ -70,7 +96,7 @@ def _cpu_slab(dist, group, v, t, origin, dx, dims, exact_band, world, rank):
     ni, nj, _ = dims
     sess = _lib.CpuSlab(world, rank, *dims)
     sess.band(v, t, origin, dx, exact_band)
-    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+    ranks = _group_ranks(dist, group)
     for s in range(16):
         below = sess.upstream_is_below(s)
         up = rank - 1 if below else rank + 1
@@ -113,7 +139,7 @@ def make_level_set3(vertices, triangles, origin, dx: float, ni: int, nj: int, nk
     if gather_to is None:
         return phi, kb, ke
     ctl = _control_group(dist, group)
-    ranks = dist.get_process_group_ranks(group) if group is not None else list(range(world))
+    ranks = _group_ranks(dist, group)
     parts = [None] * world if rank == gather_to else None
     dist.gather_object(np.asfortranarray(phi), parts, dst=ranks[gather_to], group=ctl)
     if rank != gather_to:

@@ -1,9 +1,14 @@
 """Host-side mesh and .sdf file I/O (the callers either side of the hot path).
 
-These restate the reference's loaders/writers with bulk numpy I/O instead of
+* ``load_mesh``  -- the library's native loaders (include/sdfgen_meshio.h,
+  csrc/meshio.cpp: whole-file read, OBJ parsed in parallel line chunks, correctly
+  rounded from_chars floats, update_minmax bounds in file order).  ``load_mesh_py``
+  is the line-by-line Python restatement kept as the tests' second opinion.
+
+These restate the reference's loaders/writers with bulk I/O instead of
 per-value stream calls:
 
-* ``load_mesh``  -- common/mesh_io.cpp:29-48 dispatch on extension;
+* ``load_mesh_py``  -- common/mesh_io.cpp:29-48 dispatch on extension;
   binary STL common/mesh_io_stl.cpp:98-173 (no vertex de-duplication:
   vertices 3t, 3t+1, 3t+2 per facet), ASCII STL :179-303, format detection
   :42-92, OBJ common/mesh_io_obj.cpp:21-157 (fan triangulation :115-121).
@@ -41,12 +46,21 @@ def _parse_f32(tok: str) -> np.float32:
 
 
 def _bounds(v: np.ndarray):
-    if v.shape[0] == 0:
-        mn = np.full(3, _FLT_MAX, np.float32)
-        mx = np.full(3, -_FLT_MAX, np.float32)
-    else:
-        mn = np.fmin.reduce(v, axis=0).astype(np.float32)
-        mx = np.fmax.reduce(v, axis=0).astype(np.float32)
+    """update_minmax over the vertices in order (common/util.h:299-303): a value that lowers
+    the minimum does not also raise the maximum, NaN never updates either."""
+    mn = np.full(3, _FLT_MAX, np.float32)
+    mx = np.full(3, -_FLT_MAX, np.float32)
+    for c in range(3):
+        x = v[:, c].astype(np.float32)
+        if x.size == 0:
+            continue
+        # prefix minimum BEFORE each vertex; vertex k lowers the minimum iff x_k < that
+        pre = np.minimum.accumulate(np.concatenate([[_FLT_MAX], np.where(np.isnan(x), _FLT_MAX, x)]))[:-1]
+        lowers = x < pre
+        mn[c] = np.float32(np.nanmin(np.concatenate([[_FLT_MAX], x])))
+        cand = x[~lowers & ~np.isnan(x)]
+        if cand.size:
+            mx[c] = max(np.float32(-_FLT_MAX), np.float32(cand.max()))
     return (tuple(float(a) for a in mn), tuple(float(a) for a in mx))
 
 
@@ -143,7 +157,22 @@ def _load_obj(path: str):
 def load_mesh(filename: str):
     """Load an OBJ or STL mesh -> (vertices (N,3) f32, triangles (M,3) u32, bounds).
 
-    Mirrors python/sdfgen_py.cpp:101-157 (``sdfgen.load_mesh``)."""
+    Mirrors python/sdfgen_py.cpp:101-157 (``sdfgen.load_mesh``): bounds are the loader's
+    min_box / max_box (update_minmax over the vertices in file order)."""
+    from . import _lib
+    path = os.fspath(filename)
+    ext = os.path.splitext(path)[1].lower()
+    if not os.path.isfile(path) or ext not in (".obj", ".stl"):
+        raise RuntimeError(f"Failed to load mesh: {path}")
+    try:
+        v, t, b, _ = _lib.mesh_load(path)
+    except RuntimeError as e:
+        raise RuntimeError(f"Failed to load mesh: {path} ({e})") from e
+    return v, t, (tuple(float(a) for a in b[:3]), tuple(float(a) for a in b[3:]))
+
+
+def load_mesh_py(filename: str):
+    """Python restatement of the reference loaders (slow; the tests' cross-check of load_mesh)."""
     path = os.fspath(filename)
     ext = os.path.splitext(path)[1].lower()
     if not os.path.isfile(path):

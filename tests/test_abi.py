@@ -14,7 +14,7 @@ from sdfgenfast_amd import _lib
 
 def declared_functions():
     names = set()
-    for h in ("sdfgen_hip.h", "sdfgen_cpu.h"):
+    for h in ("sdfgen_hip.h", "sdfgen_cpu.h", "sdfgen_meshio.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"^\s*(?:int|void)\s+(sdfgen_\w+)\s*\(", src, flags=re.M))
@@ -41,7 +41,7 @@ def test_cxx_dropin_symbols_exported():
 
 
 def test_abi_version_and_device_count():
-    assert _lib.lib.sdfgen_hip_abi_version() == 1
+    assert _lib.lib.sdfgen_hip_abi_version() == 2
     assert _lib.device_count() >= 0
 
 

@@ -50,6 +50,41 @@ def test_cpu_slabs_over_gloo_match_oracle(tmp_path, world, dims):
     assert bits_equal(got, want), diff_report(got, want, dx)
 
 
+def _subgroup_worker(rank, world, port, dims, result_path):
+    """3 processes; ranks 1 and 2 form a gloo subgroup and split the grid between them
+    (group-local ranks 0 and 1); rank 0 takes no part."""
+    import torch.distributed as dist
+    from sdfgenfast_amd import distributed as D
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        sub = dist.new_group(ranks=[1, 2], backend="gloo")   # collective over the whole world
+        if rank in (1, 2):
+            v, t = meshgen.bumpy_sphere(40, 17)
+            o, dx = meshgen.grid_mode2b(v, *(max(d, 8) for d in dims), 2)
+            phi, kb, ke = D.make_level_set3(v, t, o, dx, *dims, 1, backend="cpu", group=sub, gather_to=1)
+            if rank == 2:   # group rank 1 holds the gathered grid
+                assert (kb, ke) == (0, dims[2])
+                np.save(result_path, np.asfortranarray(phi))
+            else:
+                assert (kb, ke) == D.slab_range(dims[2], 2, 0)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cpu_slabs_on_a_subgroup(tmp_path):
+    """A 2-of-3-rank subgroup: group-local ranks, neighbours and gather target map to the
+    right global ranks."""
+    dims = (16, 14, 18)
+    path = str(tmp_path / "phi.npy")
+    tmp.spawn(_subgroup_worker, args=(3, _free_port(), dims, path), nprocs=3, join=True)
+    v, t = meshgen.bumpy_sphere(40, 17)
+    o, dx = meshgen.grid_mode2b(v, *(max(d, 8) for d in dims), 2)
+    want = np.asfortranarray(O.make_level_set3(v, t, o, dx, *dims, 1))
+    got = np.load(path)
+    assert bits_equal(got, want), diff_report(got, want, dx)
+
+
 def test_cpu_slab_session_single_process_chain():
     """Drive all slabs of a grid from one process, handing the planes on by hand."""
     from sdfgenfast_amd import _lib

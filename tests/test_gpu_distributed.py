@@ -65,19 +65,23 @@ def _bench_two_ranks(*extra):
 
 
 def test_bench_two_ranks_zslab_parity():
-    """bench.py --mode zslab under torch.distributed.run, 2 ranks on one GPU: bit-exact."""
-    res = _bench_two_ranks("--mode", "zslab", "--no-zslab")
-    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "zslab2" and res["scaling"] == "strong"
+    """bench.py --mode zslab under torch.distributed.run, 2 ranks on one GPU: bit-exact headline."""
+    res = _bench_two_ranks("--mode", "zslab", "--no-side")
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "zslab2" and res["scaling"] == "strong", res
     assert res["parity"] == "bit-exact vs reference (sha256 of phi)", res
-    assert "zslab" not in res
+    assert "zslab_c4" not in res and "zslab_error" not in res
+    assert res["efficiency"] > 0 and res["sweep_impl"] == 2
 
 
-def test_bench_two_ranks_replicas_with_zslab_child():
-    """Default multi-rank mode: replicas (weak scaling) plus the Z-slab side measurement
-    run as a child torch.distributed job; both bit-exact."""
-    res = _bench_two_ranks("--zslab-workload", "c2_sphere70k_128")
-    assert res["config"]["parallelism"] == "replicas2" and res["scaling"] == "weak", res
+def test_bench_two_ranks_default_line():
+    """Default N > 1 line: Z-slab headline with its efficiency, the second grid's Z-slab run and
+    the replicas run as side objects; every one bit-exact."""
+    res = _bench_two_ranks("--c4-workload", "c2_sphere70k_128")
+    assert res["config"]["parallelism"] == "zslab2" and res["scaling"] == "strong", res
     assert res["parity"] == "bit-exact vs reference (sha256 of phi)", res
-    zs = res["zslab"]
+    zs = res["zslab_c4"]
     assert "error" not in zs, zs
     assert zs["parallelism"] == "zslab2" and zs["parity"] == "bit-exact vs reference (sha256 of phi)", zs
+    assert zs["efficiency"] > 0
+    rep = res["replicas"]
+    assert rep["parallelism"] == "replicas2" and rep["parity"] == "bit-exact vs reference (sha256 of phi)", rep

@@ -46,13 +46,17 @@ def test_slabs_one_process_match_oracle(nslabs, dims):
         sl.connect_local(slabs[s - 1] if s > 0 else None, slabs[s + 1] if s < nslabs - 1 else None)
     dv, dt = _hiprt.DeviceBuffer.from_array(v), _hiprt.DeviceBuffer.from_array(t)
     outs = [_hiprt.DeviceBuffer(ni * nj * (sl.k_end - sl.k_begin) * 4) for sl in slabs]
+    for sl_ in slabs:   # every slab set up before any slab's kernels run
+        sl_.prepare(t.shape[0])
     for sl, d in zip(slabs, outs):
         sl.enqueue(dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx, 1, _lib.LAYOUT_ARRAY3, d.ptr)
     profs = [sl.finish(v.shape[0]) for sl in slabs]
     got = np.concatenate([d.download(np.float32, ni * nj * (sl.k_end - sl.k_begin)) for sl, d in zip(slabs, outs)])
     got = got.reshape((ni, nj, nk), order="F")
     assert [sl.k_begin for sl in slabs][0] == 0 and slabs[-1].k_end == nk
-    assert all(p["sweep_impl"] == 3 for p in profs)
+    impl = 1 if os.environ.get("SDFGEN_SLAB_SPARSE") == "0" else 2   # diagnostics may turn parts off
+    multi = 0 if os.environ.get("SDFGEN_TILE_MULTI") == "0" else 8
+    assert all(p["sweep_impl"] == impl and p["slabs"] == nslabs and p["tile_multi"] == multi for p in profs)
     assert bits_equal(got, want), diff_report(got, want, dx)
 
 
@@ -69,6 +73,8 @@ def test_slab_kfast_layout_and_host_run():
     from sdfgenfast_amd import _hiprt
     dv, dt = _hiprt.DeviceBuffer.from_array(v), _hiprt.DeviceBuffer.from_array(t)
     outs = [_hiprt.DeviceBuffer(ni * nj * (sl.k_end - sl.k_begin) * 4) for sl in slabs]
+    for sl_ in slabs:   # every slab set up before any slab's kernels run
+        sl_.prepare(t.shape[0])
     for sl, d in zip(slabs, outs):
         sl.enqueue(dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx, 1, _lib.LAYOUT_KFAST, d.ptr)
     for sl in slabs:
@@ -126,10 +132,10 @@ def test_slabs_ipc_one_process_per_slab_match_oracle(nslabs, dims):
     for p in procs:
         p.start()
     try:
-        handles = dict(q_out.get(timeout=300) for _ in range(nslabs))
+        handles = dict(q_out.get(timeout=100) for _ in range(nslabs))
         for q in q_ins:
             q.put(handles)
-        parts = sorted(res.get(timeout=300) for _ in range(nslabs))
+        parts = sorted(res.get(timeout=100) for _ in range(nslabs))
     finally:
         for p in procs:
             p.join(timeout=120)
@@ -139,7 +145,7 @@ def test_slabs_ipc_one_process_per_slab_match_oracle(nslabs, dims):
     v, t, o, dx, (ni, nj, nk) = _mesh(dims=dims)
     want = np.asfortranarray(O.make_level_set3(v, t, o, dx, ni, nj, nk, 1))
     got = np.concatenate([np.frombuffer(b, np.float32) for _, _, _, b, _ in parts]).reshape((ni, nj, nk), order="F")
-    assert [p[4] for p in parts] == [3] * nslabs
+    assert [p[4] for p in parts] == [2] * nslabs
     assert bits_equal(got, want), diff_report(got, want, dx)
 
 
