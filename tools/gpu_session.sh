@@ -20,7 +20,7 @@ step() {  # name timeout cmd...
 }
 rocminfo 2>/dev/null | grep -m1 -E "gfx950" || echo "no gfx950 in rocminfo"
 if [ "$what" = tests ] || [ "$what" = all ]; then
-  step pytest_gpu 1500 python -m pytest tests -m gpu -x -q "$@"
+  step pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread "$@"
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [ "$what" = bench ] || [ "$what" = all ]; then
@@ -28,7 +28,7 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
 fi
 if [ "$what" = prof ] || [ "$what" = all ]; then
   rm -rf gpurun_out/prof
-  step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-zslab
+  step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-side
   find gpurun_out/prof -name "*stats*" | head
 fi
 echo "=== session done"

@@ -8,7 +8,7 @@ W=${1:-c3_sphere1m_256}
 C=${2:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES"}
 rm -rf gpurun_out/pmc_sq
 timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc_sq -o run -- \
-  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-verify --no-zslab --workload $W > gpurun_out/pmc_sq.log 2>&1
+  python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-verify --no-side --workload $W > gpurun_out/pmc_sq.log 2>&1
 python3 - "$W" <<'PY'
 import csv, glob, sys
 from collections import defaultdict
