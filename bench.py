@@ -338,7 +338,13 @@ def main():
 
     from sdfgenfast_amd import _hiprt, _lib  # noqa: F401
 
-    dev = local_rank % max(_lib.device_count(), 1)   # = local_rank on a node with a GPU per rank
+    ndev = max(_lib.device_count(), 1)
+    dev = local_rank % ndev   # = local_rank on a node with a GPU per rank
+    shared = world > ndev     # a rehearsal with several slabs per GPU (one-GPU box)
+    if shared and "SDFGEN_TILE_GRID" not in os.environ:
+        # Co-resident slabs: the persistent first-pass grids must fit on the one GPU together
+        # (3 tile workgroups per CU), or a waiting slab can hold every CU its upstream slab needs.
+        os.environ["SDFGEN_TILE_GRID"] = str(max(32, 3 * 256 // ((world + ndev - 1) // ndev) - 32))
     _hiprt.set_device(dev)
     step_us = step_latency(dev) if rank == 0 else None
 
@@ -411,7 +417,8 @@ def main():
             "dtype": "f32",
             "data": "synthetic (deterministic 1M-triangle bumpy UV-sphere, sdfgenfast_amd/meshgen.py)",
             "config": {"workload": args.workload, "grid": [ni, nj, nk], "triangles": r["triangles"],
-                       "exact_band": 1, "parallelism": parallelism, "inputs": "HBM-resident"},
+                       "exact_band": 1, "parallelism": parallelism, "inputs": "HBM-resident",
+                       "ranks_per_gpu": (world + ndev - 1) // ndev},
             "roofline": roofline(r, step_us, args.workload),
             "valu": valu(r, args.workload) if world == 1 else None,
             "phases_ms": r["phases"],
