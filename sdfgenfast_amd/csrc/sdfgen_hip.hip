@@ -590,7 +590,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->wf.grid_override = gr ? atoi(gr) : 0;
         const char *ld = getenv("SDFGEN_TILE_LEAD");      // diagnostics: inter-wave lead
         ws->wf.lead_override = ld ? atoi(ld) : -1;
-        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 32, st));
+        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 128, st));
     }
     const char *nsw_env = getenv("SDFGEN_DEBUG_NSWEEPS");   // diagnostics: stop after n sweeps
     const int nsweeps = nsw_env ? atoi(nsw_env) : 16;
@@ -679,13 +679,13 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     }
     HIPCHK(hipEventRecord(ev[20], st));
     int flag = 0, wf_err = 0;
-    unsigned long long evals = 0, wf_stats[4] = {0, 0, 0, 0}, sp_ctl[SP_NCTL] = {};
+    unsigned long long evals = 0, wf_stats[16] = {}, sp_ctl[SP_NCTL] = {};
     if (sparse_sweeps)
         HIPCHK(hipMemcpyAsync(sp_ctl, ws->sp.ctl, sizeof(sp_ctl), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     if (impl == 1 && ws->wf.ctrl) {
         HIPCHK(hipMemcpyAsync(&wf_err, ws->wf.ctrl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, 32, hipMemcpyDeviceToHost, st));
+        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, sizeof(wf_stats), hipMemcpyDeviceToHost, st));
     }
     HIPCHK(hipMemcpyAsync(&evals, ws->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -712,6 +712,15 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sweep_launches = launches;
     p.sweep_impl = impl;
     p.band_evals = evals;
+#ifdef ST_STEP_PROF
+    if (ws->wf.count) {
+        const double steps = (double)(wf_stats[8] + wf_stats[9] + wf_stats[10]);
+        fprintf(stderr, "step profile: %.0f wave-steps (single no-eval %.3f, single eval %.3f, multi %.3f, pairs/multi %.1f); "
+                        "cycles/step poll %.0f mask %.0f eval %.0f writeback %.0f\n", steps, wf_stats[8] / steps,
+                wf_stats[9] / steps, wf_stats[10] / steps, wf_stats[10] ? (double)wf_stats[11] / wf_stats[10] : 0.0,
+                wf_stats[4] / steps, wf_stats[5] / steps, wf_stats[6] / steps, wf_stats[7] / steps);
+    }
+#endif
     p.sweep_evals = wf_stats[0];
     p.sweep_stalls = wf_stats[1];
     p.helper_polls = wf_stats[2];
@@ -724,6 +733,18 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
 #ifdef SP_JACOBI_COUNT
     fprintf(stderr, "jacobi candidates %llu lane-passes %llu (slot use %.3f)\n", sp_ctl[SP_DIAG], sp_ctl[SP_DIAG + 1],
             sp_ctl[SP_DIAG + 1] ? sp_ctl[SP_DIAG] / (2.0 * sp_ctl[SP_DIAG + 1]) : 0.0);
+#endif
+#ifdef SP_PROF
+    if (sparse_sweeps)
+        fprintf(stderr, "repair profile (%d sweeps): evaluations %llu, claims %llu; wave iterations with work %llu "
+                        "(max per wave per sweep-sum %llu), cycles per such iteration %.0f (eval %.0f)\n",
+                sparse_sweeps, sp_ctl[SP_RUNS], sp_ctl[SP_ENQ], sp_ctl[SP_DIAG + 2], sp_ctl[SP_DIAG + 3],
+                sp_ctl[SP_DIAG + 2] ? (double)sp_ctl[SP_DIAG] / sp_ctl[SP_DIAG + 2] : 0.0,
+                sp_ctl[SP_DIAG + 2] ? (double)sp_ctl[SP_DIAG + 1] / sp_ctl[SP_DIAG + 2] : 0.0);
+    if (sparse_sweeps && sp_ctl[SP_DIAG + 2])
+        fprintf(stderr, "  per such iteration: loop top %.0f, X store+order %.0f, retire+requests %.0f, append %.0f\n",
+                (double)sp_ctl[SP_DIAGX] / sp_ctl[SP_DIAG + 2], (double)sp_ctl[SP_DIAGX + 1] / sp_ctl[SP_DIAG + 2],
+                (double)sp_ctl[SP_DIAGX + 2] / sp_ctl[SP_DIAG + 2], (double)sp_ctl[SP_DIAGX + 3] / sp_ctl[SP_DIAG + 2]);
 #endif
     p.sparse_rechecks = sp_ctl[SP_RUNS];
     p.sparse_claims = sp_ctl[SP_ENQ];

@@ -28,8 +28,10 @@
 //     a runner reads labels only after the request it retires was observed: the first
 //     evaluation retires just the request that handed it the cell (written after the
 //     label that caused it), and every further round retires what its atomicSub saw.
-//   * the high half of ctl[SP_QUEUE] counts queued or running work items (it grows in
-//     the same atomic as the ring tail); workers leave when it is 0.
+//   * the work list is cut into shards; a wave appends to and takes from its home shard only.
+//     The high half of a shard's tail word counts its queued or running work items (it grows
+//     in the same atomic as the ring tail, one atomic per wave and iteration for all lanes'
+//     new items and finished ones); the shard's workers leave when it is 0.
 // Every spin is bounded (watchdog -> error bit, reported by the host).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -42,18 +44,24 @@
 
 namespace sdfhip {
 
-// ctl[SP_QUEUE]: work items appended to the ring (low 32 bits) and work items queued or
+// A shard's tail word: work items appended to its ring (low 32 bits) and work items queued or
 // running (high 32 bits) in ONE word, so an append is one atomic round trip.
 // ctl layout: words 0..7 accumulate over the call (error bits, statistics); from SP_QUEUE
-// on everything is reset before each sweep: the work-list counters, then the Jacobi list
-// counters of SP_JPARTS parts, one 128-byte line each (a shared line serialises the
-// atomics of the whole grid: 1.4 ms per sweep at 256^3, measured).
+// on everything is reset before each sweep: the Z-slab words, the Jacobi list counters of
+// SP_JPARTS parts, one 128-byte line each (a shared line serialises the atomics of the whole
+// grid: 1.4 ms per sweep at 256^3, measured), then the work-list shards' words.
 // Z-slab words (reset per sweep): SP_INHEAD reservations of the inbound ring, SP_INDONE inbound
 // lanes finished, SP_EXIT waves exited, SP_OUTTAIL entries this slab appended to the downstream
 // slab's inbound ring.
 enum { SP_ERR = 0, SP_ENQ = 1, SP_RUNS = 2, SP_DIAG = 4, SP_QUEUE = 8, SP_HEAD = 9, SP_INHEAD = 10, SP_INDONE = 11,
        SP_EXIT = 12, SP_OUTTAIL = 13,
-       SP_JPARTS = 64, SP_JSTRIDE = 16, SP_JLIST = 16, SP_NCTL = SP_JLIST + SP_JPARTS * SP_JSTRIDE };
+       SP_JPARTS = 64, SP_JSTRIDE = 16, SP_JLIST = 16, SP_SHARD0 = SP_JLIST + SP_JPARTS * SP_JSTRIDE,
+       SP_SHSTRIDE = 32, SP_MAXNQ = 16, SP_DIAGX = SP_SHARD0 + SP_MAXNQ * SP_SHSTRIDE,
+       SP_NCTL = SP_DIAGX + 8 };   // SP_DIAGX..: diagnostics accumulated over the call
+// Work-list shards (SP_NQ): shard s has its own ring (P.queue + s * P.cap), its tail+pending word
+// ctl[SP_SHARD0 + s * SP_SHSTRIDE] and its head word 16 words (128 bytes) further.  A wave appends
+// to and takes from its home shard only, so every shard is a closed system that drains on its
+// own; one shared word serialised the returning atomics of all 64 repair waves.
 // SP_ERR bits: 1 repair watchdog, 2 ring overflow, 4 Jacobi list overflow, 8 inbound ring overflow
 // (Z-slab), 16 a neighbour slab's flag never came (Z-slab watchdog).
 // Z-slab flag words in the uncached communication block (sdfgen_hip.hip SlabSession), one 128-byte
@@ -66,6 +74,28 @@ constexpr unsigned long long SP_TAIL_LIMIT = 0xF0000000ull;   // appends per swe
 constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
 constexpr int SP_WORKERS = 512;              // max one-wave workgroups of the repair kernel
 constexpr int SP_WORKERS_DEFAULT = 128;
+#ifndef SP_NQ
+#define SP_NQ 8        // work-list shards (fewer where NQ rings of n cells would pass 2^31 entries)
+#endif
+static_assert(SP_NQ >= 1 && SP_NQ <= 16 && (SP_NQ & (SP_NQ - 1)) == 0, "work-list shards: a power of two <= 16");
+// shards for n cells: every shard's ring holds n cells (it can never overflow), all rings together
+// at most 2^31 entries (8 GB)
+inline unsigned sp_shards(unsigned long long n)
+{
+    unsigned q = SP_NQ;
+    while (q > 1 && (unsigned long long)q * n > (1ull << 31)) q >>= 1;
+    return q;
+}
+#ifndef SP_QUAD
+#define SP_QUAD 0      // 1: the repair evaluates each cell with a quad of lanes (sp_eval_quad; measured slower)
+#endif
+constexpr unsigned SP_INLANES = SP_QUAD ? 16u : 64u;   // Z-slab inbound-ring workers (workgroup 0's leaders)
+#ifndef SP_TERM_EVERY
+#define SP_TERM_EVERY 1u   // an idle lane reads the shared queue word every SP_TERM_EVERY empty polls (power of 2)
+#endif
+#ifndef SP_IDLE_SLEEP
+#define SP_IDLE_SLEEP 2
+#endif
 
 // the reference's 8 sweep directions in pass order (cpu_lib/makelevelset3.cpp:243-291)
 constexpr int SP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
@@ -80,7 +110,8 @@ struct SpParams {
     unsigned *jlist;                   // Jacobi list: SP_JPARTS parts of jcap cells
     unsigned long long jcap;
     unsigned long long *ctl;           // SP_* counters
-    unsigned long long cap;            // ring slots
+    unsigned long long cap;            // ring slots per work-list shard
+    unsigned nq;                       // work-list shards (sp_shards)
     unsigned long long n;              // cells
     float ox, oy, oz, dx;
     int ni, nj, nk;
@@ -255,12 +286,76 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
 }
 
 
+// The repair's evaluation with a QUAD of lanes per cell (lanes 4g..4g+3, all active, same cell):
+// each lane takes the candidates of rank r and r + 4 (r = lane & 3) in one packed pass, and the
+// quad applies the <= 7 distances in rank (= q) order after DPP broadcasts -- one ptd pass per
+// evaluation instead of max(count)/2 dependent passes of gathers and ptd per wave.
+// Every lane of the quad returns the same result.
+__device__ __forceinline__ int sp_quad_bcast(int v, int src)   // lane `src` of each quad to all four
+{
+    switch (src) {
+    case 0: return __builtin_amdgcn_update_dpp(v, v, 0x00, 0xF, 0xF, false);
+    case 1: return __builtin_amdgcn_update_dpp(v, v, 0x55, 0xF, 0xF, false);
+    case 2: return __builtin_amdgcn_update_dpp(v, v, 0xAA, 0xF, 0xF, false);
+    default: return __builtin_amdgcn_update_dpp(v, v, 0xFF, 0xF, 0xF, false);
+    }
+}
+
+template <bool SLAB>
+__device__ __forceinline__ unsigned long long sp_eval_quad(const SpParams &P, const unsigned long long *L, int i, int j,
+                                                           int k, size_t c, unsigned long long own)
+{
+    const unsigned r = threadIdx.x & 3u;
+    int lab[7];
+    const unsigned f = sp_mask<true, SLAB>(P, L, i, j, k, c, own, lab);
+    // this lane's candidates: ranks r and r + 4 (bits cleared from the bottom, branch-free)
+    const unsigned m1 = f & (f - 1u), m2 = m1 & (m1 - 1u), m3 = m2 & (m2 - 1u), m4 = m3 & (m3 - 1u);
+    const unsigned m5 = m4 & (m4 - 1u), m6 = m5 & (m5 - 1u), m7 = m6 & (m6 - 1u);
+    const unsigned fa = r == 0u ? f : (r == 1u ? m1 : (r == 2u ? m2 : m3));
+    const unsigned fb = r == 0u ? m4 : (r == 1u ? m5 : (r == 2u ? m6 : m7));
+    const bool has_a = fa != 0u, has_b = fb != 0u;
+    const int qa = has_a ? __builtin_ctz(fa) : 0, qb = has_b ? __builtin_ctz(fb) : qa;
+    int ta = lab[0], tb = lab[0];
+#pragma unroll
+    for (int q = 1; q < 7; ++q) {   // static indices: no register-array indexing
+        ta = (qa == q) ? lab[q] : ta;
+        tb = (qb == q) ? lab[q] : tb;
+    }
+    float phi = __uint_as_float((uint32_t)(own >> 32));
+    int ct = lbl_of((uint32_t)own);
+    bool changed = false;
+    if (__any(has_a)) {
+        const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
+        const size_t ba = 3 * SDF_CHK(26, (has_a ? ta : 0), 0, P.ntri),
+                     bb = 3 * SDF_CHK(26, (has_b ? tb : (has_a ? ta : 0)), 0, P.ntri);
+        const float4 a0 = P.soup[ba], a1 = P.soup[ba + 1], a2 = P.soup[ba + 2];
+        const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
+        float da, db;
+        ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w, gx,
+                  mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), b2.w, da, db);
+        const int n = __popc(f);   // the same in all four lanes
+#pragma unroll
+        for (int kk = 0; kk < 7; ++kk) {   // rank order = the reference's check order (:143-149)
+            const float dk = __int_as_float(sp_quad_bcast(__float_as_int(kk < 4 ? da : db), kk & 3));
+            const int tk = sp_quad_bcast(kk < 4 ? ta : tb, kk & 3);
+            const bool take = (kk < n) & (dk < phi);
+            phi = take ? dk : phi;
+            ct = take ? tk : ct;
+            changed = changed | take;
+        }
+    }
+    if (!changed) return own;
+    return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
+}
+
 // Request rechecks of the downstream neighbours of (i,j,k) (the cells whose upwind set
-// contains it).  Returns the first cell this call took ownership of when `claim`, so
-// the caller can run it itself; the others are queued.
+// contains it): the 7 request counters in one round trip.  The cells whose counter moved 0 -> 1
+// are this lane's to queue: slot bits in *qmask, cells in tgt[].  With `claim`, the first of them
+// is returned instead (the caller runs it itself, depth-first) and left out of *qmask.
 // Only cells of planes [k_lo, k_hi) are requested (a Z-slab's own planes; for an upstream slab's
 // cell -- an inbound entry -- that is the cells of this slab's first plane).
-__device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i, int j, int k, size_t c, bool claim)
+__device__ __forceinline__ size_t sp_request_collect(const SpParams &P, int i, int j, int k, size_t c, bool claim,
+                                                     unsigned *qmask, size_t (&tgt)[7])
 {
     const bool ii = P.di > 0 ? i + 1 <= P.ni - 1 : i - 1 >= 0;
     const bool jj = P.dj > 0 ? j + 1 <= P.nj - 1 : j - 1 >= 0;
@@ -268,8 +363,6 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
     const bool k0 = k >= P.k_lo && k < P.k_hi;   // targets in this cell's own plane
     const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
     const long long cc = (long long)c;
-    // all requests in flight at once, then one reservation for the cells to queue
-    size_t tgt[7];
     unsigned old[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
@@ -281,23 +374,47 @@ __device__ __forceinline__ size_t sp_request_downstream(const SpParams &P, int i
         old[q] = ok ? atomicAdd(&P.req[SDF_CHK(24, tgt[q], P.c_lo, P.c_lo + P.n)], 1u) : 1u;
     }
     size_t mine = ~(size_t)0;
-    unsigned nq = 0;
+    unsigned qm = 0;
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
         if (old[q] != 0u) continue;
         if (claim && mine == ~(size_t)0) mine = tgt[q];
-        else ++nq;
+        else qm |= 1u << q;
     }
-    if (nq) {
-        // pending and tail grow together, so no item is visible to a worker before it counts
-        const unsigned long long old_q = atomicAdd(&P.ctl[SP_QUEUE], nq * SP_PENDING_ONE + nq);
-        unsigned long long t = old_q & 0xffffffffull;
-        if (t + nq > SP_TAIL_LIMIT) atomicOr(&P.ctl[SP_ERR], 2ull);
-#pragma unroll
-        for (int q = 0; q < 7; ++q)
-            if (old[q] == 0u && tgt[q] != mine) sp_st32(P.queue + (t++) % P.cap, (unsigned)(tgt[q] + 1));
-    }
+    *qmask = qm;
     return mine;
+}
+
+// Wave-level (every lane of the wave calls it, uniformly): queue the cells each lane collected
+// (qmask / tgt of sp_request_collect) and retire `fin` lanes' work items, in ONE atomic on the
+// shared queue word per wave.  Its low half is the ring tail, its high half the work items queued
+// or running: new items count before this wave's finished ones stop counting, so the count cannot
+// touch 0 while work remains.  (One atomic per lane saturated the word: ~100 returning atomics per
+// microsecond on one address at 256^3 -- DESIGN.md §4.)
+__device__ __forceinline__ void sp_append_wave(const SpParams &P, unsigned shard, unsigned qmask, const size_t (&tgt)[7],
+                                               bool fin)
+{
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned nq = __popc(qmask);
+    const unsigned long long b0 = __ballot(nq & 1u), b1 = __ballot(nq & 2u), b2 = __ballot(nq & 4u),
+                             bf = __ballot(fin);
+    if (!(b0 | b1 | b2 | bf)) return;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned pre = (unsigned)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+    const unsigned long long tot = (unsigned long long)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    const unsigned long long nfin = (unsigned long long)__popcll(bf);
+    unsigned long long t0 = 0;
+    if (lane == 0) {
+        // pending += tot - nfin, tail += tot (two's complement in the high half)
+        const unsigned long long old_q = atomicAdd(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE], (tot - nfin) * SP_PENDING_ONE + tot);
+        t0 = old_q & 0xffffffffull;
+        if (t0 + tot > SP_TAIL_LIMIT) atomicOr(&P.ctl[SP_ERR], 2ull);
+    }
+    t0 = ((unsigned long long)(unsigned)__shfl((int)(t0 >> 32), 0) << 32) | (unsigned)__shfl((int)t0, 0);
+    unsigned long long t = t0 + pre;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+        if ((qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + (t++) % P.cap, (unsigned)(tgt[q] + 1));
 }
 
 // Pass 1 of the sparse sweep: every cell against the labels of S, in two kernels.
@@ -332,7 +449,7 @@ __device__ __forceinline__ void sp_push(const SpParams &P, int i, int j, int k, 
 }
 
 template <bool SLAB = false>
-__device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32)
+__device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32, unsigned *qmask, size_t (&tgt)[7])
 {
     const int i = (int)(c32 % (unsigned)P.ni);
     const unsigned r = c32 / (unsigned)P.ni;
@@ -342,7 +459,7 @@ __device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32)
     P.X[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = y;
     if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) {
         if (SLAB) sp_push(P, i, j, k, c32, (uint32_t)y);
-        sp_request_downstream(P, i, j, k, c32, false);
+        sp_request_collect(P, i, j, k, c32, false, qmask, tgt);
     }
 }
 
@@ -437,35 +554,69 @@ __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
     const unsigned long long cnt0 = P.ctl[SP_JLIST + part * SP_JSTRIDE];
     const unsigned long long cnt = cnt0 < P.jcap ? cnt0 : P.jcap;
     const unsigned *list = P.jlist + (size_t)part * P.jcap;
-    for (unsigned long long x = (unsigned long long)(blockIdx.x / SP_JPARTS) * blockDim.x + threadIdx.x; x < cnt;
-         x += (unsigned long long)(gridDim.x / SP_JPARTS) * blockDim.x)
-        sp_jacobi_cell<SLAB>(P, list[x]);
+    const unsigned lane = threadIdx.x & 63;
+    // wave-uniform trip count: the queue appends are wave-level (sp_append_wave)
+    for (unsigned long long x = (unsigned long long)(blockIdx.x / SP_JPARTS) * blockDim.x + threadIdx.x; x - lane < cnt;
+         x += (unsigned long long)(gridDim.x / SP_JPARTS) * blockDim.x) {
+        unsigned qmask = 0;
+        size_t tgt[7];
+        if (x < cnt) sp_jacobi_cell<SLAB>(P, list[x], &qmask, tgt);
+        sp_append_wave(P, (unsigned)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (P.nq - 1u)), qmask, tgt, false);
+    }
 }
 
-// Pass 2: drain the recheck work list.  One lane = one worker; chains are followed
-// depth-first by the lane that changed the upstream cell.  Written as a flat loop in
-// which every lane does at most one poll or one evaluation per iteration: a lane
-// spinning on an empty slot must never hold back (SIMT reconvergence) lanes of its own
-// wave whose work would fill that slot.
+// Pass 2: drain the recheck work list.  One QUAD of lanes = one worker (SP_QUAD; otherwise one
+// lane): the quad's first lane runs the queue protocol, all four evaluate its cell together
+// (sp_eval_quad).  Chains are followed depth-first by the worker that changed the upstream cell.
+// Written as a flat loop in which every worker does at most one poll or one evaluation per
+// iteration: a lane spinning on an empty slot must never hold back (SIMT reconvergence) lanes of
+// its own wave whose work would fill that slot.
 //
 // Z-slab: the lanes of workgroup 0 also drain the inbound ring (cells of the upstream slab's last
 // plane that changed label; their live halo words are already in place): each entry becomes
 // requests for this slab's first-plane cells downstream of it.  A lane's inbound part is finished
 // once the upstream slab's repair has ended (its DONE flag) and every entry it appended (its
-// COUNT) is taken; local lanes stop only after all 64 inbound lanes finished and nothing is queued
+// COUNT) is taken; local lanes stop only after all SP_INLANES inbound lanes finished and nothing is queued
 // or running.  The last wave to leave tells the downstream slab (COUNT, then DONE) and the
 // upstream slab (DONE: our pushes into its halo for its next sweep are in place).
 template <bool SLAB>
 __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 {
     constexpr size_t NONE = ~(size_t)0;
+    const bool leader = !SP_QUAD || (threadIdx.x & 3u) == 0u;   // runs the queue protocol
     unsigned long long runs = 0, claims = 0, h = 0, h_in = 0;
     size_t e = NONE, next = NONE;
     unsigned rq = 1;
-    bool done = false, waiting = false, in_wait = false;
-    bool in_role = SLAB && P.in_ring != nullptr && blockIdx.x == 0;   // still draining the inbound ring
+    bool done = !leader, waiting = false, in_wait = false;
+    bool in_role = SLAB && P.in_ring != nullptr && blockIdx.x == 0 && leader;   // still draining the inbound ring
     unsigned spins = 0, in_spins = 0;
+#ifdef SP_PROF   // diagnostics: cycles of the iterations in which a lane evaluated, and how many
+    unsigned long long pf_work = 0, pf_eval = 0, pf_it = 0, pf_t0 = 0, pf_t1 = 0, pf_top = 0, pf_st = 0, pf_req = 0, pf_t2 = 0, pf_app = 0;
+#endif
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned long long lane_lt = (1ull << lane) - 1ull;
+    const unsigned shard = blockIdx.x & (P.nq - 1u);   // this wave's home work-list shard
     for (;;) {
+#ifdef SP_PROF
+        pf_t0 = clock64();
+#endif
+        unsigned qmask = 0;   // cells this lane queues this iteration (sp_append_wave below)
+        size_t tgt[7];
+        bool fin = false;     // this lane's work item ended this iteration
+        {
+            // queue tickets for every lane that needs one: ONE atomic on the head word per wave
+            const bool want = !done && e == NONE && !waiting && !(SLAB && in_role);
+            const unsigned long long wm = __ballot(want);
+            if (wm) {
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE + 16], (unsigned long long)__popcll(wm));
+                base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 0) << 32) | (unsigned)__shfl((int)base, 0);
+                if (want) {
+                    h = base + (unsigned long long)__popcll(wm & lane_lt);
+                    waiting = true;
+                }
+            }
+        }
         if (SLAB && in_role && e == NONE) {
             if (!in_wait) {
                 h_in = atomicAdd(&P.ctl[SP_INHEAD], 1ull);
@@ -480,7 +631,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 const unsigned u = v - 1;   // an upstream cell: its downstream cells here are queued
                 const int iu = (int)(u % (unsigned)P.ni);
                 const unsigned ru = u / (unsigned)P.ni;
-                sp_request_downstream(P, iu, (int)(ru % (unsigned)P.nj), (int)(ru / (unsigned)P.nj), u, false);
+                sp_request_collect(P, iu, (int)(ru % (unsigned)P.nj), (int)(ru / (unsigned)P.nj), u, false, &qmask, tgt);
             } else if (__hip_atomic_load(P.flags + (SP_FL_DONE + P.up_side) * SP_FL_STRIDE, __ATOMIC_RELAXED,
                                          __HIP_MEMORY_SCOPE_SYSTEM) >= P.epoch &&
                        h_in >= __hip_atomic_load(P.flags + (SP_FL_COUNT + P.up_side) * SP_FL_STRIDE,
@@ -494,11 +645,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 atomicAdd(&P.ctl[SP_INDONE], 1ull);
             }
         } else if (!done && e == NONE) {
-            if (!waiting) {
-                h = atomicAdd(&P.ctl[SP_HEAD], 1ull);
-                waiting = true;
-            }
-            unsigned *slot = P.queue + h % P.cap;
+            unsigned *slot = P.queue + (size_t)shard * P.cap + h % P.cap;
             const unsigned v = sp_ld32(slot);
             if (v) {
                 sp_st32(slot, 0u);
@@ -507,65 +654,112 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 rq = 1;
                 waiting = false;
                 spins = 0;
-            } else if ((!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= 64ull) &&
-                       (sp_ld64(&P.ctl[SP_QUEUE]) >> 32) == 0ull) {
+            } else if ((++spins & (SP_TERM_EVERY - 1u)) == 0u &&
+                       (!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= (unsigned long long)SP_INLANES) &&
+                       (sp_ld64(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE]) >> 32) == 0ull) {
                 done = true;   // nothing queued or running anywhere (nor to come): no slot can fill any more
-            } else if (++spins > SP_WATCHDOG) {
+            } else if (spins > SP_WATCHDOG) {
                 atomicOr(&P.ctl[SP_ERR], 1ull);
                 done = true;
             }
         }
-        if (e != NONE) {
-            // one evaluation of cell e, retiring `rq` requests
-            const int i = (int)((unsigned)e % (unsigned)P.ni);
-            const unsigned r0 = (unsigned)e / (unsigned)P.ni;
-            const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
-#ifdef SP_RT_PROBE   // diagnostics: N extra dependent device-scope round trips per evaluation
-            {
-                size_t e2 = e;
-#pragma unroll
-                for (int i_ = 0; i_ < SP_RT_PROBE; ++i_) e2 += (size_t)(sp_ld64(P.X + e2) & 0ull);
-                e = e2;
-            }
+#ifdef SP_PROF
+        const bool pf_any = __any(e != NONE);
+        pf_t1 = clock64();
+        if (pf_any) pf_top += pf_t1 - pf_t0;
 #endif
-            const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, e, P.c_lo, P.c_lo + P.n));
+        // the worker's cell, in every lane of its quad
+        size_t eq = e;
+        if (SP_QUAD) {
+            const int lead = (int)(threadIdx.x & 63u & ~3u);
+            eq = ((size_t)(unsigned)__shfl((int)((unsigned long long)e >> 32), lead) << 32) |
+                 (size_t)(unsigned)__shfl((int)(unsigned)e, lead);
+        }
+        if (eq != NONE) {
+            // one evaluation of cell eq, retiring `rq` requests (the leader's part below)
+            const int i = (int)((unsigned)eq % (unsigned)P.ni);
+            const unsigned r0 = (unsigned)eq / (unsigned)P.ni;
+            const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
+            const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, eq, P.c_lo, P.c_lo + P.n));
 #ifdef SP_NOEVAL_RECHECK   // diagnostics: the work list's own cost (no evaluation, no relabel)
             const unsigned long long y = cur;
 #else
-            const unsigned long long y = sp_eval<true, SLAB>(P, P.X, i, j, k, e, P.S[e]);
+            const unsigned long long y = SP_QUAD ? sp_eval_quad<SLAB>(P, P.X, i, j, k, eq, P.S[eq])
+                                                 : sp_eval<true, SLAB>(P, P.X, i, j, k, eq, P.S[eq]);
 #endif
-            ++runs;
-            const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
-            if (y != cur) {
-                sp_st64(P.X + e, y);
-                if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
-            }
-            if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
-            // retire e's requests and ask for the downstream rechecks in one round trip
-            const unsigned old = atomicSub(P.req + e, rq);
-            if (relabel) {
-                const size_t m = sp_request_downstream(P, i, j, k, e, next == NONE);
-                if (m != NONE) next = m;
-            }
-            if (old == rq) {   // no request arrived meanwhile: e is settled
-                if (next != NONE) {
-                    e = next;   // the work item's pending count carries over to the claimed cell
-                    next = NONE;
-                    rq = 1;
-                    ++claims;
-                } else {
-                    e = NONE;
-                    sp_order();
-                    atomicSub(&P.ctl[SP_QUEUE], SP_PENDING_ONE);
+#ifdef SP_PROF
+            pf_eval += clock64() - pf_t1;   // (lanes of the wave: the same scalar clock)
+#endif
+            if (leader) {
+                ++runs;
+                const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
+#ifdef SP_PROF
+                pf_t2 = clock64();
+#endif
+                if (y != cur) {
+                    sp_st64(P.X + e, y);
+                    if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
                 }
-            } else {
-                rq = old - rq;   // evaluate again for the requests that arrived meanwhile
-                sp_order();
+#ifdef SP_PROF
+                pf_st += clock64() - pf_t2;
+                pf_t2 = clock64();
+#endif
+                if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
+                // retire e's requests and ask for the downstream rechecks in one round trip
+                const unsigned old = atomicSub(P.req + e, rq);
+                if (relabel) {
+                    const size_t m = sp_request_collect(P, i, j, k, e, next == NONE, &qmask, tgt);
+                    if (m != NONE) next = m;
+                }
+#ifdef SP_PROF
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                pf_req += clock64() - pf_t2;
+#endif
+                if (old == rq) {   // no request arrived meanwhile: e is settled
+                    if (next != NONE) {
+                        e = next;   // the work item's pending count carries over to the claimed cell
+                        next = NONE;
+                        rq = 1;
+                        ++claims;
+                    } else {
+                        e = NONE;
+                        fin = true;   // retired in sp_append_wave, in the same atomic as the wave's new items
+                    }
+                } else {
+                    rq = old - rq;   // evaluate again for the requests that arrived meanwhile
+                    sp_order();
+                }
             }
         }
+#ifdef SP_PROF
+        const unsigned long long pf_ta = clock64();
+#endif
+        sp_append_wave(P, shard, qmask, tgt, fin);
+#ifdef SP_PROF
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (pf_any) pf_app += clock64() - pf_ta;
+#endif
+#ifdef SP_PROF
+        if (pf_any) {
+            pf_work += clock64() - pf_t0;
+            ++pf_it;
+        }
+#endif
         if (__all(done)) break;
-        if (!__any(e != NONE)) __builtin_amdgcn_s_sleep(2);
+        if (SP_IDLE_SLEEP && !__any(e != NONE)) __builtin_amdgcn_s_sleep(SP_IDLE_SLEEP);
     }
+#ifdef SP_PROF
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(&P.ctl[SP_DIAG], pf_work);
+        atomicAdd(&P.ctl[SP_DIAG + 1], pf_eval);
+        atomicAdd(&P.ctl[SP_DIAG + 2], pf_it);
+        atomicMax(&P.ctl[SP_DIAG + 3], pf_it);
+        atomicAdd(&P.ctl[SP_DIAGX], pf_top);
+        atomicAdd(&P.ctl[SP_DIAGX + 1], pf_st);
+        atomicAdd(&P.ctl[SP_DIAGX + 2], pf_req);
+        atomicAdd(&P.ctl[SP_DIAGX + 3], pf_app);
+    }
+#endif
     if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
     if (claims) atomicAdd(&P.ctl[SP_ENQ], claims);
     if (SLAB) {
@@ -715,7 +909,7 @@ inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, hipStream_t
 {
     const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
     if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;
-    if (sp_grow(&W.queue, &W.cap_queue, cap, true, st)) return -5;
+    if (sp_grow(&W.queue, &W.cap_queue, sp_shards(n) * cap, true, st)) return -5;
     if (!W.ctl) {
         if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
         if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
@@ -738,13 +932,13 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     const int di = SP_DIRS[sweep % 8][0], dj = SP_DIRS[sweep % 8][1], dk = SP_DIRS[sweep % 8][2];
     const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
     if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;      // stays all-zero between sweeps
-    if (sp_grow(&W.queue, &W.cap_queue, cap, true, st)) return -5; // slots are reset when consumed
+    if (sp_grow(&W.queue, &W.cap_queue, sp_shards(n) * cap, true, st)) return -5; // slots are reset when consumed
     if (!W.ctl) {
         if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
         if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
     }
     // per sweep: reset the list counters; error bits and statistics accumulate over the call
-    if (hipMemsetAsync(W.ctl + SP_QUEUE, 0, (SP_NCTL - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
+    if (hipMemsetAsync(W.ctl + SP_QUEUE, 0, (SP_DIAGX - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
         return -4;
     blocks = (n + 255) / 256;
     if (blocks > 16384) blocks = 16384;
@@ -763,6 +957,7 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.jcap = jcap;
     P.ctl = W.ctl;
     P.cap = cap;
+    P.nq = sp_shards(n);
     P.n = n;
     P.c_lo = c_lo;
     P.ox = origin[0];

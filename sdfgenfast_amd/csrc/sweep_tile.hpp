@@ -68,6 +68,9 @@ namespace sdfhip {
 #ifndef ST_WORK_PRIO
 #define ST_WORK_PRIO 2   // compute waves' issue priority while stepping (0 while they wait)
 #endif
+#ifndef ST_TWIN
+#define ST_TWIN 1      // twin lanes split each cell's candidates (needs 32-cell compute waves)
+#endif
 #ifndef ST_WPE_DEF
 #define ST_WPE_DEF 3   // waves per SIMD the register budget must allow
 #endif
@@ -82,6 +85,7 @@ constexpr int ST_RO = ST_RO_DEF;
 constexpr int ST_RH = ST_RH_DEF;
 constexpr int ST_G = ST_G_DEF;
 static_assert(ST_NCW >= 1 && ST_NCW <= 3 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
+static_assert(!ST_TWIN || ST_CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
 typedef int i4v __attribute__((ext_vector_type(4)));
 static_assert((ST_RR & (ST_RR - 1)) == 0 && ST_RR >= 8, "ring slots: power of two >= 8 (RR = 4 measured wrong results: no lead left between the waves)");
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
@@ -387,26 +391,32 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         if (TRACE && P.trace && tid == 0) P.trace[8 * task] = wall_clock64();
         if (wave < ST_NCW) {
             // ======================= compute waves =======================
-            // Wave w owns the 16 columns cl in {2w, 2w+1}; lanes 0..15 are cells, all 64 lanes
-            // evaluate.  Wave w steps h only after wave w-1 finished step h-1 (its column
-            // cl-1 results) and at most 4 steps ahead of wave w+1 (8-slot ring).
+            // Wave w owns the ST_CLW c-columns from ST_CLW * w on: lanes 0..31 are its 32 cells.
+            // Wave w steps h only after wave w-1 finished step h-1 (its column cl-1 results) and
+            // at most RR-4 steps ahead of wave w+1 (ring slots).  ST_TWIN: lane L + 32 is the twin
+            // of cell lane L -- same cell, same candidate mask; L evaluates the cell's 1st, 3rd, ...
+            // candidate and L + 32 its 2nd, 4th, ..., handed back with one v_permlane32_swap.
             const int w = wave;
             const bool cell_lane = L < ST_CPW;
             const int bl = L & (ST_T - 1), cl = ST_CLW * w + ((L >> 3) & (ST_CLW - 1));
             const int col_id = cl * ST_T + bl;
             const int b = b0 + bl, c = c0 + cl;
-            const bool col = cell_lane && b < P.B && c < P.ce;
+            const bool colx = b < P.B && c < P.ce;   // the cell (cell lane or twin)
+            const bool col = cell_lane && colx;
             __builtin_amdgcn_s_setprio(ST_WORK_PRIO);
-            int nb_base[7], nb_stride[7], nb_mask[7];
+            // neighbour q's entry at step h: nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]) (ring slots are
+            // ST_NCOL = 64 entries apart, halo slots 1)
+            int nb_base[7], nb_sh[7], nb_mask[7];
             {
+                static_assert(ST_NCOL == 64, "ring slot stride is a shift by 6");
                 auto ring = [&](int q, int lbl, int lcl) {
                     nb_base[q] = ST_RING0 + lcl * ST_T + lbl;
-                    nb_stride[q] = ST_NCOL;
+                    nb_sh[q] = 6;
                     nb_mask[q] = ST_RR - 1;
                 };
                 auto halo = [&](int q, int s) {
                     nb_base[q] = ST_HALO0 + s * ST_RH;
-                    nb_stride[q] = 1;
+                    nb_sh[q] = 0;
                     nb_mask[q] = ST_RH - 1;
                 };
                 ring(0, bl, cl);                                              // (a-1, b,   c)
@@ -423,9 +433,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                       hsC = (bl == 0 && cl == 0) ? 2 * ST_T : ST_NSTREAM;
             unsigned polls = 0;
             unsigned long long t_wait = 0, w_own = 0, w_halo = 0, t_comp = 0, c_comp = 0;   // trace-only
+#ifdef ST_STEP_PROF   // diagnostics: where a compute step's cycles go (host prints the sums)
+            unsigned long long sp_c[4] = {0, 0, 0, 0}, sp_n[4] = {0, 0, 0, 0}, sp_t = 0;
+#endif
             for (int h = 0; h < nsteps; ++h) {
+#ifdef ST_STEP_PROF
+                sp_t = clock64();
+#endif
                 const int a = h - bl - cl;
                 const bool act = col && a >= 0 && a < P.A;
+                const bool actx = (ST_TWIN ? colx : col) && a >= 0 && a < P.A;   // the lanes that evaluate
                 // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
                 unsigned long long tw0 = 0;
                 for (;;) {
@@ -466,6 +483,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
                 if (TRACE && tw0) t_wait += wall_clock64() - tw0;
                 if (h >= nsteps) break;
+#ifdef ST_STEP_PROF
+                { const unsigned long long t_ = clock64(); sp_c[0] += t_ - sp_t; sp_t = t_; }
+#endif
                 const unsigned long long tc0 = (TRACE && P.trace) ? wall_clock64() : 0ull;
                 const unsigned long long cc0 = (TRACE && P.trace) ? clock64() : 0ull;
                 polls = 0;
@@ -476,8 +496,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 int lab[7], ent[7];
                 unsigned fmask = 0;
                 const int e_own = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id;
-                if (act) {
-                    const float4 o0 = s_ent[3 * e_own], o1 = s_ent[3 * e_own + 1];
+                if (actx) {
+                    const float4 o0 = s_ent[__umul24(e_own, 3)], o1 = s_ent[__umul24(e_own, 3) + 1];
                     own_w = __float_as_uint(o0.w);
                     ct = lbl_of(own_w);
                     phi = o1.w;
@@ -486,8 +506,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         const int aq = (q & 1) == 0 ? a - 1 : a;   // q = 0,2,4,6 read a-1
-                        ent[q] = nb_base[q] + (aq & nb_mask[q]) * nb_stride[q];
-                        const uint32_t wq = __float_as_uint(s_ent[3 * ent[q]].w);
+                        ent[q] = nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]);
+                        const uint32_t wq = __float_as_uint(s_ent[__umul24(ent[q], 3)].w);   // (full-rate 24-bit multiply)
                         lab[q] = lbl_of(wq);
                         lcq[q] = lc_of(wq);
                     }
@@ -517,9 +537,64 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     for (int i_ = 0; i_ < ST_VALU_PROBE; ++i_) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x_));
                 }
 #endif
+#if ST_TWIN
+                // ---- candidates in pairs: the cell lane takes the lowest remaining one, its twin
+                //      the next; one ptd per lane per pass, applied in the reference check order
+                //      (strict '<', first minimum wins: cpu_lib/makelevelset3.cpp:94-99, 143-149) ----
+#ifdef ST_STEP_PROF
+                { const unsigned long long t_ = clock64(); sp_c[1] += t_ - sp_t; sp_t = t_; }
+                {
+                    const unsigned mp_ = __popc(fmask);
+                    if (!__any(mp_ != 0u)) ++sp_n[0];
+                    else if (!__any(mp_ > 2u)) ++sp_n[1];
+                    else ++sp_n[2];
+                }
+#endif
+                // at most 2 candidates per cell (else the wave-wide compaction below balances them)
+                if (__all(__popc(fmask) <= 2u)) {
+                    const f3 gx = st_gx(P, a, b, c);
+                    unsigned fm = cell_lane ? fmask : (fmask & (fmask - 1u));
+                    if (__any(fm != 0u)) {
+                        const bool has = fm != 0u;
+                        const int qa = has ? __builtin_ctz(fm) : 0;
+                        int e1 = ent[0], t1 = lab[0];
+#pragma unroll
+                        for (int q = 1; q < 7; ++q) {   // static indices: no register-array indexing
+                            e1 = (qa == q) ? ent[q] : e1;
+                            t1 = (qa == q) ? lab[q] : t1;
+                        }
+                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
+                        const float d1 = ptd_wave(gx, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v3), v3.w);
+                        n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;
+#ifdef ST_STEP_PROF
+                        ++sp_n[3];
+#endif
+                        // the twin's distance, label and entry (lanes 32..63 -> 0..31)
+                        const float d2 = __uint_as_float(
+                            __builtin_amdgcn_permlane32_swap(__float_as_uint(d1), __float_as_uint(d1), false, false)[1]);
+                        const int t2 = (int)__builtin_amdgcn_permlane32_swap((unsigned)t1, (unsigned)t1, false, false)[1];
+                        const int e2 = (int)__builtin_amdgcn_permlane32_swap((unsigned)e1, (unsigned)e1, false, false)[1];
+                        const bool has2 = (fm & (fm - 1u)) != 0u;   // (cell lane) the pair's second candidate
+                        const bool take1 = has & (d1 < phi);
+                        phi = take1 ? d1 : phi;
+                        ct = take1 ? t1 : ct;
+                        win = take1 ? e1 : win;
+                        const bool take2 = has2 & (d2 < phi);
+                        phi = take2 ? d2 : phi;
+                        ct = take2 ? t2 : ct;
+                        win = take2 ? e2 : win;
+                    }
+                } else {
+                fmask = cell_lane ? fmask : 0u;   // the compaction below lists each cell's pairs once
+#endif
                 // ---- at most one candidate per cell (the common case away from the surface):
                 //      each cell lane evaluates its own, no compaction and no LDS exchange ----
                 const bool single = __all(__popc(fmask) <= 1);
+#if defined(ST_STEP_PROF) && !ST_TWIN
+                { const unsigned long long t_ = clock64(); sp_c[1] += t_ - sp_t; sp_t = t_; }
+                if (single) ++sp_n[__any(fmask != 0u) ? 1 : 0];
+                else ++sp_n[2];
+#endif
                 if (single) {
                     if (fmask) {
                         int e1 = ent[0], t1 = lab[0];
@@ -529,8 +604,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                                 e1 = ent[q];
                                 t1 = lab[q];
                             }
-                        const float4 v3 = s_ent[3 * e1 + 2];
-                        const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]),
+                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
+                        const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]),
                                                st_xyz(v3), v3.w);
                         if (d < phi) {
                             phi = d;
@@ -564,18 +639,21 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
                                             c0 + ST_CLW * w + (l2 >> 3));
                         float d1, d2;
-                        const float4 v13 = s_ent[3 * e1 + 2], v23 = s_ent[3 * e2 + 2];
-                        ptd_wave2(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(v13), v13.w, g2,
-                                  st_xyz(s_ent[3 * e2]), st_xyz(s_ent[3 * e2 + 1]), st_xyz(v23), v23.w, d1, d2);
+                        const float4 v13 = s_ent[__umul24(e1, 3) + 2], v23 = s_ent[__umul24(e2, 3) + 2];
+                        ptd_wave2(g1, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v13), v13.w, g2,
+                                  st_xyz(s_ent[__umul24(e2, 3)]), st_xyz(s_ent[__umul24(e2, 3) + 1]), st_xyz(v23), v23.w, d1, d2);
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
                         s_d[w][has2 ? ((p2 >> 6) & 7) * ST_CPW + l2 : 7 * ST_CPW + L] = d2;
                     } else {
                         s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] =
-                            ptd_wave(g1, st_xyz(s_ent[3 * e1]), st_xyz(s_ent[3 * e1 + 1]), st_xyz(s_ent[3 * e1 + 2]),
-                                     s_ent[3 * e1 + 2].w);
+                            ptd_wave(g1, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(s_ent[__umul24(e1, 3) + 2]),
+                                     s_ent[__umul24(e1, 3) + 2].w);
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
+#if defined(ST_STEP_PROF) && !ST_TWIN
+                sp_n[3] += (unsigned long long)total;
+#endif
                 // ---- apply in the reference check order: strict '<', first minimum wins ----
                 if (act) {   // branch-free: all 7 slots read at once, non-candidates masked out
                     float dq[7];
@@ -590,16 +668,22 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                 }
                 }
+#if ST_TWIN
+                }
+#endif
+#ifdef ST_STEP_PROF
+                { const unsigned long long t_ = clock64(); sp_c[2] += t_ - sp_t; sp_t = t_; }
+#endif
                 if (act) {
                     const int src = win < 0 ? e_own : win;
-                    const float4 w0 = s_ent[3 * src];
-                    const float4 w1 = s_ent[3 * src + 1], w2 = s_ent[3 * src + 2];
+                    const float4 w0 = s_ent[__umul24(src, 3)];
+                    const float4 w1 = s_ent[__umul24(src, 3) + 1], w2 = s_ent[__umul24(src, 3) + 2];
                     const int slot = ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id;
                     // a winner always carries a new label (the own label is never a candidate)
                     const uint32_t w_new = win >= 0 ? lo_word(ct, P.sweep + 1) : own_w;
-                    s_ent[3 * slot] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
-                    s_ent[3 * slot + 1] = w1;
-                    s_ent[3 * slot + 2] = w2;
+                    s_ent[__umul24(slot, 3)] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
+                    s_ent[__umul24(slot, 3) + 1] = w1;
+                    s_ent[__umul24(slot, 3) + 2] = w2;
                     if (win >= 0)
                         P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
                             ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
@@ -618,10 +702,19 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 }
                 lds_drain();
                 if (L == 0) lds_st(&s_hdr[1 + w], h + 1);
+#ifdef ST_STEP_PROF
+                sp_c[3] += clock64() - sp_t;
+#endif
                 if (TRACE && P.trace && w == 0 && L == 0 && (h == 0 || h == nsteps / 2))
                     P.trace[8 * task + (h == 0 ? 1 : 2)] = wall_clock64();
             }
             __builtin_amdgcn_s_setprio(0);
+#ifdef ST_STEP_PROF
+            if (P.stats && L == 0) {
+                for (int i_ = 0; i_ < 4; ++i_) atomicAdd(P.stats + 4 + i_, sp_c[i_]);
+                for (int i_ = 0; i_ < 4; ++i_) atomicAdd(P.stats + 8 + i_, sp_n[i_]);
+            }
+#endif
             if (TRACE && P.trace && w == 0 && L == 0) {
                 P.trace[8 * task + 3] = wall_clock64();
                 P.trace[8 * task + 4] = t_wait;
@@ -903,7 +996,7 @@ inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int
     if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A, st)) return -5;
     if (!W.ctrl) {
         if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return -5;
-        if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return -5;
+        if (hipMalloc((void **)&W.stats, 16 * sizeof(unsigned long long)) != hipSuccess) return -5;
         if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return -4;
     }
     int ti = (W.task_nJ[0] == nJ && W.task_nK[0] == nK) ? 0 : (W.task_nJ[1] == nJ && W.task_nK[1] == nK) ? 1 : -1;
@@ -1121,7 +1214,7 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc, st)) return fail(-5, "halo buffer allocation failed");
     if (!W.ctrl) {
         if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
-        if (hipMalloc((void **)&W.stats, 4 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
+        if (hipMalloc((void **)&W.stats, 16 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
         if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     }
     int ntasks = 0;

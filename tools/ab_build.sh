@@ -9,4 +9,5 @@ F="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -Iinclude -Isdfgenfast_
 $H --offload-arch=gfx950 $F -c sdfgenfast_amd/csrc/sdfgen_hip.hip -o ab/build_$1/a.o
 $H -x hip --offload-arch=gfx950 $F -c sdfgenfast_amd/csrc/cpu_backend.cpp -o ab/build_$1/b.o
 $H $F -c sdfgenfast_amd/csrc/sdfgen_unified.cpp -o ab/build_$1/c.o
+$H $F -c sdfgenfast_amd/csrc/meshio.cpp -o ab/build_$1/d.o
 $H --offload-arch=gfx950 -shared -fPIC -o ab/$1.so ab/build_$1/*.o -lpthread
