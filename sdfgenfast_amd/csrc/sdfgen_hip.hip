@@ -606,7 +606,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         const char *e = getenv("SDFGEN_SPARSE_WORKERS");   // diagnostics: repair-kernel workgroups
         // repair workgroups: fewer on small grids (256^3: 64 beat 128 by 0.25 ms; 512^3: 128
         // beat 64 by 2.2 ms -- more concurrent chains there)
-        ws->sp.workers = e ? atoi(e) : (n <= (1ull << 25) ? 64 : SP_WORKERS_DEFAULT);
+        ws->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
     }
     ws->wf.skip_seen = getenv("SDFGEN_NO_SEEN_SKIP") == nullptr;   // diagnostics
     ws->wf.clo = 0;
@@ -733,18 +733,6 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
 #ifdef SP_JACOBI_COUNT
     fprintf(stderr, "jacobi candidates %llu lane-passes %llu (slot use %.3f)\n", sp_ctl[SP_DIAG], sp_ctl[SP_DIAG + 1],
             sp_ctl[SP_DIAG + 1] ? sp_ctl[SP_DIAG] / (2.0 * sp_ctl[SP_DIAG + 1]) : 0.0);
-#endif
-#ifdef SP_PROF
-    if (sparse_sweeps)
-        fprintf(stderr, "repair profile (%d sweeps): evaluations %llu, claims %llu; wave iterations with work %llu "
-                        "(max per wave per sweep-sum %llu), cycles per such iteration %.0f (eval %.0f)\n",
-                sparse_sweeps, sp_ctl[SP_RUNS], sp_ctl[SP_ENQ], sp_ctl[SP_DIAG + 2], sp_ctl[SP_DIAG + 3],
-                sp_ctl[SP_DIAG + 2] ? (double)sp_ctl[SP_DIAG] / sp_ctl[SP_DIAG + 2] : 0.0,
-                sp_ctl[SP_DIAG + 2] ? (double)sp_ctl[SP_DIAG + 1] / sp_ctl[SP_DIAG + 2] : 0.0);
-    if (sparse_sweeps && sp_ctl[SP_DIAG + 2])
-        fprintf(stderr, "  per such iteration: loop top %.0f, X store+order %.0f, retire+requests %.0f, append %.0f\n",
-                (double)sp_ctl[SP_DIAGX] / sp_ctl[SP_DIAG + 2], (double)sp_ctl[SP_DIAGX + 1] / sp_ctl[SP_DIAG + 2],
-                (double)sp_ctl[SP_DIAGX + 2] / sp_ctl[SP_DIAG + 2], (double)sp_ctl[SP_DIAGX + 3] / sp_ctl[SP_DIAG + 2]);
 #endif
     p.sparse_rechecks = sp_ctl[SP_RUNS];
     p.sparse_claims = sp_ctl[SP_ENQ];
@@ -1089,7 +1077,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
         // second pass as Jacobi + repair per slab: the state alternates between cell and alt
         {
             const char *e = getenv("SDFGEN_SPARSE_WORKERS");
-            S->sp.workers = e ? atoi(e) : (nslab <= (1ull << 25) ? 64 : SP_WORKERS_DEFAULT);
+            S->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
         }
         // our boundary planes into the neighbours' parity-0 halo planes, then DONE
         SpExportParams E;

@@ -73,7 +73,7 @@ constexpr unsigned long long SP_PENDING_ONE = 1ull << 32;
 constexpr unsigned long long SP_TAIL_LIMIT = 0xF0000000ull;   // appends per sweep (error beyond)
 constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
 constexpr int SP_WORKERS = 512;              // max one-wave workgroups of the repair kernel
-constexpr int SP_WORKERS_DEFAULT = 128;
+constexpr int SP_WORKERS_DEFAULT = 256;   // 64-thread repair workgroups (C3: 64 -> 4.75 ms, 256 -> 4.6; C4: 128 -> 21.2, 256 -> 19.5)
 #ifndef SP_NQ
 #define SP_NQ 8        // work-list shards (fewer where NQ rings of n cells would pass 2^31 entries)
 #endif
@@ -86,13 +86,7 @@ inline unsigned sp_shards(unsigned long long n)
     while (q > 1 && (unsigned long long)q * n > (1ull << 31)) q >>= 1;
     return q;
 }
-#ifndef SP_QUAD
-#define SP_QUAD 0      // 1: the repair evaluates each cell with a quad of lanes (sp_eval_quad; measured slower)
-#endif
-constexpr unsigned SP_INLANES = SP_QUAD ? 16u : 64u;   // Z-slab inbound-ring workers (workgroup 0's leaders)
-#ifndef SP_TERM_EVERY
-#define SP_TERM_EVERY 1u   // an idle lane reads the shared queue word every SP_TERM_EVERY empty polls (power of 2)
-#endif
+constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup 0's lanes)
 #ifndef SP_IDLE_SLEEP
 #define SP_IDLE_SLEEP 2
 #endif
@@ -285,68 +279,6 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
     return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
 }
 
-
-// The repair's evaluation with a QUAD of lanes per cell (lanes 4g..4g+3, all active, same cell):
-// each lane takes the candidates of rank r and r + 4 (r = lane & 3) in one packed pass, and the
-// quad applies the <= 7 distances in rank (= q) order after DPP broadcasts -- one ptd pass per
-// evaluation instead of max(count)/2 dependent passes of gathers and ptd per wave.
-// Every lane of the quad returns the same result.
-__device__ __forceinline__ int sp_quad_bcast(int v, int src)   // lane `src` of each quad to all four
-{
-    switch (src) {
-    case 0: return __builtin_amdgcn_update_dpp(v, v, 0x00, 0xF, 0xF, false);
-    case 1: return __builtin_amdgcn_update_dpp(v, v, 0x55, 0xF, 0xF, false);
-    case 2: return __builtin_amdgcn_update_dpp(v, v, 0xAA, 0xF, 0xF, false);
-    default: return __builtin_amdgcn_update_dpp(v, v, 0xFF, 0xF, 0xF, false);
-    }
-}
-
-template <bool SLAB>
-__device__ __forceinline__ unsigned long long sp_eval_quad(const SpParams &P, const unsigned long long *L, int i, int j,
-                                                           int k, size_t c, unsigned long long own)
-{
-    const unsigned r = threadIdx.x & 3u;
-    int lab[7];
-    const unsigned f = sp_mask<true, SLAB>(P, L, i, j, k, c, own, lab);
-    // this lane's candidates: ranks r and r + 4 (bits cleared from the bottom, branch-free)
-    const unsigned m1 = f & (f - 1u), m2 = m1 & (m1 - 1u), m3 = m2 & (m2 - 1u), m4 = m3 & (m3 - 1u);
-    const unsigned m5 = m4 & (m4 - 1u), m6 = m5 & (m5 - 1u), m7 = m6 & (m6 - 1u);
-    const unsigned fa = r == 0u ? f : (r == 1u ? m1 : (r == 2u ? m2 : m3));
-    const unsigned fb = r == 0u ? m4 : (r == 1u ? m5 : (r == 2u ? m6 : m7));
-    const bool has_a = fa != 0u, has_b = fb != 0u;
-    const int qa = has_a ? __builtin_ctz(fa) : 0, qb = has_b ? __builtin_ctz(fb) : qa;
-    int ta = lab[0], tb = lab[0];
-#pragma unroll
-    for (int q = 1; q < 7; ++q) {   // static indices: no register-array indexing
-        ta = (qa == q) ? lab[q] : ta;
-        tb = (qb == q) ? lab[q] : tb;
-    }
-    float phi = __uint_as_float((uint32_t)(own >> 32));
-    int ct = lbl_of((uint32_t)own);
-    bool changed = false;
-    if (__any(has_a)) {
-        const f3 gx = mk3((float)i * P.dx + P.ox, (float)j * P.dx + P.oy, (float)k * P.dx + P.oz);
-        const size_t ba = 3 * SDF_CHK(26, (has_a ? ta : 0), 0, P.ntri),
-                     bb = 3 * SDF_CHK(26, (has_b ? tb : (has_a ? ta : 0)), 0, P.ntri);
-        const float4 a0 = P.soup[ba], a1 = P.soup[ba + 1], a2 = P.soup[ba + 2];
-        const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
-        float da, db;
-        ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w, gx,
-                  mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), b2.w, da, db);
-        const int n = __popc(f);   // the same in all four lanes
-#pragma unroll
-        for (int kk = 0; kk < 7; ++kk) {   // rank order = the reference's check order (:143-149)
-            const float dk = __int_as_float(sp_quad_bcast(__float_as_int(kk < 4 ? da : db), kk & 3));
-            const int tk = sp_quad_bcast(kk < 4 ? ta : tb, kk & 3);
-            const bool take = (kk < n) & (dk < phi);
-            phi = take ? dk : phi;
-            ct = take ? tk : ct;
-            changed = changed | take;
-        }
-    }
-    if (!changed) return own;
-    return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
-}
 
 // Request rechecks of the downstream neighbours of (i,j,k) (the cells whose upwind set
 // contains it): the 7 request counters in one round trip.  The cells whose counter moved 0 -> 1
@@ -565,41 +497,38 @@ __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
     }
 }
 
-// Pass 2: drain the recheck work list.  One QUAD of lanes = one worker (SP_QUAD; otherwise one
-// lane): the quad's first lane runs the queue protocol, all four evaluate its cell together
-// (sp_eval_quad).  Chains are followed depth-first by the worker that changed the upstream cell.
-// Written as a flat loop in which every worker does at most one poll or one evaluation per
-// iteration: a lane spinning on an empty slot must never hold back (SIMT reconvergence) lanes of
-// its own wave whose work would fill that slot.
+// Pass 2: drain the recheck work list.  One lane = one worker; chains are followed depth-first by
+// the lane that changed the upstream cell.  Written as a flat loop in which every lane does at
+// most one poll or one evaluation per iteration: a lane spinning on an empty slot must never hold
+// back (SIMT reconvergence) lanes of its own wave whose work would fill that slot.  Queue traffic
+// is per wave: one ticket atomic for all lanes that need work, one read of the shard's tail word
+// (lanes poll their slot only once the tail has passed it, and the same word says when the shard
+// has drained), one append atomic for all lanes' new items and finished ones.
 //
 // Z-slab: the lanes of workgroup 0 also drain the inbound ring (cells of the upstream slab's last
 // plane that changed label; their live halo words are already in place): each entry becomes
 // requests for this slab's first-plane cells downstream of it.  A lane's inbound part is finished
 // once the upstream slab's repair has ended (its DONE flag) and every entry it appended (its
-// COUNT) is taken; local lanes stop only after all SP_INLANES inbound lanes finished and nothing is queued
-// or running.  The last wave to leave tells the downstream slab (COUNT, then DONE) and the
+// COUNT) is taken; local lanes stop only after all SP_INLANES inbound lanes finished and nothing is
+// queued or running.  The last wave to leave tells the downstream slab (COUNT, then DONE) and the
 // upstream slab (DONE: our pushes into its halo for its next sweep are in place).
 template <bool SLAB>
 __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 {
     constexpr size_t NONE = ~(size_t)0;
-    const bool leader = !SP_QUAD || (threadIdx.x & 3u) == 0u;   // runs the queue protocol
     unsigned long long runs = 0, claims = 0, h = 0, h_in = 0;
     size_t e = NONE, next = NONE;
     unsigned rq = 1;
-    bool done = !leader, waiting = false, in_wait = false;
-    bool in_role = SLAB && P.in_ring != nullptr && blockIdx.x == 0 && leader;   // still draining the inbound ring
+    bool done = false, waiting = false, in_wait = false;
+    bool in_role = SLAB && P.in_ring != nullptr && blockIdx.x == 0;   // still draining the inbound ring
     unsigned spins = 0, in_spins = 0;
-#ifdef SP_PROF   // diagnostics: cycles of the iterations in which a lane evaluated, and how many
-    unsigned long long pf_work = 0, pf_eval = 0, pf_it = 0, pf_t0 = 0, pf_t1 = 0, pf_top = 0, pf_st = 0, pf_req = 0, pf_t2 = 0, pf_app = 0;
-#endif
     const unsigned lane = threadIdx.x & 63;
     const unsigned long long lane_lt = (1ull << lane) - 1ull;
     const unsigned shard = blockIdx.x & (P.nq - 1u);   // this wave's home work-list shard
+    unsigned long long *const q_tail = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];   // pending << 32 | tail
+    unsigned long long *const q_head = q_tail + 16;
+    unsigned *const ring = P.queue + (size_t)shard * P.cap;
     for (;;) {
-#ifdef SP_PROF
-        pf_t0 = clock64();
-#endif
         unsigned qmask = 0;   // cells this lane queues this iteration (sp_append_wave below)
         size_t tgt[7];
         bool fin = false;     // this lane's work item ended this iteration
@@ -609,13 +538,19 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             const unsigned long long wm = __ballot(want);
             if (wm) {
                 unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE + 16], (unsigned long long)__popcll(wm));
+                if (lane == 0) base = atomicAdd(q_head, (unsigned long long)__popcll(wm));
                 base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 0) << 32) | (unsigned)__shfl((int)base, 0);
                 if (want) {
                     h = base + (unsigned long long)__popcll(wm & lane_lt);
                     waiting = true;
                 }
             }
+        }
+        // the shard's tail word, read once for the wave's waiting lanes
+        unsigned long long qw = 0;
+        if (__any(!done && e == NONE && waiting && !(SLAB && in_role))) {
+            if (lane == 0) qw = sp_ld64(q_tail);
+            qw = ((unsigned long long)(unsigned)__shfl((int)(qw >> 32), 0) << 32) | (unsigned)__shfl((int)qw, 0);
         }
         if (SLAB && in_role && e == NONE) {
             if (!in_wait) {
@@ -645,121 +580,65 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 atomicAdd(&P.ctl[SP_INDONE], 1ull);
             }
         } else if (!done && e == NONE) {
-            unsigned *slot = P.queue + (size_t)shard * P.cap + h % P.cap;
-            const unsigned v = sp_ld32(slot);
+            // the slot is read only once the tail has passed it (appended; its store may still land)
+            const unsigned v = h < (qw & 0xffffffffull) ? sp_ld32(ring + h % P.cap) : 0u;
             if (v) {
-                sp_st32(slot, 0u);
+                sp_st32(ring + h % P.cap, 0u);
                 e = SDF_CHK(28, v - 1, P.c_lo, P.c_lo + P.n);
                 next = NONE;
                 rq = 1;
                 waiting = false;
                 spins = 0;
-            } else if ((++spins & (SP_TERM_EVERY - 1u)) == 0u &&
-                       (!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= (unsigned long long)SP_INLANES) &&
-                       (sp_ld64(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE]) >> 32) == 0ull) {
-                done = true;   // nothing queued or running anywhere (nor to come): no slot can fill any more
-            } else if (spins > SP_WATCHDOG) {
+            } else if ((qw >> 32) == 0ull && (!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= (unsigned long long)SP_INLANES)) {
+                done = true;   // nothing queued or running in this shard (nor to come): no slot can fill any more
+            } else if (++spins > SP_WATCHDOG) {
                 atomicOr(&P.ctl[SP_ERR], 1ull);
                 done = true;
             }
         }
-#ifdef SP_PROF
-        const bool pf_any = __any(e != NONE);
-        pf_t1 = clock64();
-        if (pf_any) pf_top += pf_t1 - pf_t0;
-#endif
-        // the worker's cell, in every lane of its quad
-        size_t eq = e;
-        if (SP_QUAD) {
-            const int lead = (int)(threadIdx.x & 63u & ~3u);
-            eq = ((size_t)(unsigned)__shfl((int)((unsigned long long)e >> 32), lead) << 32) |
-                 (size_t)(unsigned)__shfl((int)(unsigned)e, lead);
-        }
-        if (eq != NONE) {
-            // one evaluation of cell eq, retiring `rq` requests (the leader's part below)
-            const int i = (int)((unsigned)eq % (unsigned)P.ni);
-            const unsigned r0 = (unsigned)eq / (unsigned)P.ni;
+        if (e != NONE) {
+            // one evaluation of cell e, retiring `rq` requests
+            const int i = (int)((unsigned)e % (unsigned)P.ni);
+            const unsigned r0 = (unsigned)e / (unsigned)P.ni;
             const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
-            const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, eq, P.c_lo, P.c_lo + P.n));
+            const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, e, P.c_lo, P.c_lo + P.n));
 #ifdef SP_NOEVAL_RECHECK   // diagnostics: the work list's own cost (no evaluation, no relabel)
             const unsigned long long y = cur;
 #else
-            const unsigned long long y = SP_QUAD ? sp_eval_quad<SLAB>(P, P.X, i, j, k, eq, P.S[eq])
-                                                 : sp_eval<true, SLAB>(P, P.X, i, j, k, eq, P.S[eq]);
+            const unsigned long long y = sp_eval<true, SLAB>(P, P.X, i, j, k, e, P.S[e]);
 #endif
-#ifdef SP_PROF
-            pf_eval += clock64() - pf_t1;   // (lanes of the wave: the same scalar clock)
-#endif
-            if (leader) {
-                ++runs;
-                const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
-#ifdef SP_PROF
-                pf_t2 = clock64();
-#endif
-                if (y != cur) {
-                    sp_st64(P.X + e, y);
-                    if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
-                }
-#ifdef SP_PROF
-                pf_st += clock64() - pf_t2;
-                pf_t2 = clock64();
-#endif
-                if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
-                // retire e's requests and ask for the downstream rechecks in one round trip
-                const unsigned old = atomicSub(P.req + e, rq);
-                if (relabel) {
-                    const size_t m = sp_request_collect(P, i, j, k, e, next == NONE, &qmask, tgt);
-                    if (m != NONE) next = m;
-                }
-#ifdef SP_PROF
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                pf_req += clock64() - pf_t2;
-#endif
-                if (old == rq) {   // no request arrived meanwhile: e is settled
-                    if (next != NONE) {
-                        e = next;   // the work item's pending count carries over to the claimed cell
-                        next = NONE;
-                        rq = 1;
-                        ++claims;
-                    } else {
-                        e = NONE;
-                        fin = true;   // retired in sp_append_wave, in the same atomic as the wave's new items
-                    }
+            ++runs;
+            const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
+            if (y != cur) {
+                sp_st64(P.X + e, y);
+                if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
+            }
+            if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
+            // retire e's requests and ask for the downstream rechecks in one round trip
+            const unsigned old = atomicSub(P.req + e, rq);
+            if (relabel) {
+                const size_t m = sp_request_collect(P, i, j, k, e, next == NONE, &qmask, tgt);
+                if (m != NONE) next = m;
+            }
+            if (old == rq) {   // no request arrived meanwhile: e is settled
+                if (next != NONE) {
+                    e = next;   // the work item's pending count carries over to the claimed cell
+                    next = NONE;
+                    rq = 1;
+                    ++claims;
                 } else {
-                    rq = old - rq;   // evaluate again for the requests that arrived meanwhile
-                    sp_order();
+                    e = NONE;
+                    fin = true;   // retired in sp_append_wave, in the same atomic as the wave's new items
                 }
+            } else {
+                rq = old - rq;   // evaluate again for the requests that arrived meanwhile
+                sp_order();
             }
         }
-#ifdef SP_PROF
-        const unsigned long long pf_ta = clock64();
-#endif
         sp_append_wave(P, shard, qmask, tgt, fin);
-#ifdef SP_PROF
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (pf_any) pf_app += clock64() - pf_ta;
-#endif
-#ifdef SP_PROF
-        if (pf_any) {
-            pf_work += clock64() - pf_t0;
-            ++pf_it;
-        }
-#endif
         if (__all(done)) break;
         if (SP_IDLE_SLEEP && !__any(e != NONE)) __builtin_amdgcn_s_sleep(SP_IDLE_SLEEP);
     }
-#ifdef SP_PROF
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&P.ctl[SP_DIAG], pf_work);
-        atomicAdd(&P.ctl[SP_DIAG + 1], pf_eval);
-        atomicAdd(&P.ctl[SP_DIAG + 2], pf_it);
-        atomicMax(&P.ctl[SP_DIAG + 3], pf_it);
-        atomicAdd(&P.ctl[SP_DIAGX], pf_top);
-        atomicAdd(&P.ctl[SP_DIAGX + 1], pf_st);
-        atomicAdd(&P.ctl[SP_DIAGX + 2], pf_req);
-        atomicAdd(&P.ctl[SP_DIAGX + 3], pf_app);
-    }
-#endif
     if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
     if (claims) atomicAdd(&P.ctl[SP_ENQ], claims);
     if (SLAB) {
