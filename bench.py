@@ -315,6 +315,8 @@ def main():
     ap.add_argument("--no-side", action="store_true", help="headline only (no zslab_c4 / replicas / host)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-latency", action="store_true",
+                    help="skip the isolated-tile step timing (profiling runs: its launches would mix into the counters)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -346,7 +348,7 @@ def main():
         # (3 tile workgroups per CU), or a waiting slab can hold every CU its upstream slab needs.
         os.environ["SDFGEN_TILE_GRID"] = str(max(32, 3 * 256 // ((world + ndev - 1) // ndev) - 32))
     _hiprt.set_device(dev)
-    step_us = step_latency(dev) if rank == 0 else None
+    step_us = step_latency(dev) if rank == 0 and not args.no_latency else None
 
     res_side = {}
     zs_err = None

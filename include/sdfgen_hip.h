@@ -137,11 +137,14 @@ int sdfgen_hip_release(void);
  * (README.md:220 lists multi-GPU as future work); SURVEY.md §8.e.
  *
  * A session owns planes k in [k_begin, k_end) of an ni x nj x nk grid (slab s of n:
- * k_begin = s*nk/n).  Band, ray parity and sign are local.  Each of the 16 sweeps runs
- * the tile wavefront on the slab; the boundary plane travels between neighbouring
- * slabs as tagged granules written straight into the neighbour's inbox (xGMI, the
- * inbox memory is mapped across processes with HIP IPC), so the wavefront pipelines
- * across GPUs inside every sweep.  Result bits equal the single-GPU / reference bits.
+ * k_begin = s*nk/n) and allocates only those planes.  Band, ray parity and sign are local.
+ * Sweeps 1-8 run as one overlapped tile-wavefront launch per slab in a schedule computed
+ * for all slabs; the boundary plane travels between neighbouring slabs as tagged granules
+ * written straight into the neighbour's inbox, so the wavefront pipelines across GPUs
+ * inside every sweep.  Sweeps 9-16 run as Jacobi + repair per slab; boundary-plane label
+ * changes are pushed into the neighbour's halo plane and inbound ring.  Everything a
+ * neighbour writes is one uncached allocation per slab (xGMI; mapped across processes
+ * with HIP IPC).  Result bits equal the single-GPU / reference bits.
  *
  * One process per GPU:   create -> export (IPC handle) -> exchange handles (e.g.
  * torch.distributed all_gather) -> connect_ipc(lower, upper) -> barrier -> run.

@@ -28,7 +28,7 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
 fi
 if [ "$what" = prof ] || [ "$what" = all ]; then
   rm -rf gpurun_out/prof
-  step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-side
+  step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-verify --no-side --no-latency
   find gpurun_out/prof -name "*stats*" | head
 fi
 echo "=== session done"

@@ -9,6 +9,6 @@ W=${1:-c3_sphere1m_256}
 for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/pmc_$c
   timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d gpurun_out/pmc_$c -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-side --workload $W > gpurun_out/pmc_$c.log 2>&1
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-side --no-latency --workload $W > gpurun_out/pmc_$c.log 2>&1
 done
-python3 tools/pmc_summary.py "$W"
+python3 tools/pmc_summary.py "$W"   # (writes profiles/ on the box; gpurun merges only gpurun_out/: rerun it here)

@@ -26,11 +26,11 @@ def main():
     for (name, grid, block), v in rows:
         out.append([name, grid, block, len(v), round(sum(v), 4), round(sum(v) / len(v), 4), round(min(v), 4),
                     round(max(v), 4), round(100 * sum(v) / total, 2)])
-    for r in out:
-        print(",".join(str(x) for x in r))
     if dst:
         with open(dst, "w", newline="") as f:
             csv.writer(f).writerows(out)
+    for r in out:
+        print(",".join(str(x) for x in r))
 
 
 if __name__ == "__main__":
