@@ -259,49 +259,95 @@ inline bool starts_ci(const char *p, const char *e, const char *kw)
 
 // ASCII STL (mesh_io_stl.cpp:179-303): keywords matched case-insensitively at the start of
 // each whitespace-trimmed line, in the reference's order; vertex lines parsed as
-// `keyword >> x >> y >> z`.  Sequential: it is a state machine and ASCII STL files are rare.
-int load_ascii_stl(const std::vector<char> &buf, sdfgen_mesh &m, char *errbuf, size_t errlen)
+// `keyword >> x >> y >> z`.  Two phases: line chunks are classified and their vertex numbers
+// parsed in parallel (the cost: 3 correctly rounded floats per vertex line), then the state
+// machine replays the line events in file order, so errors surface exactly where the
+// sequential reference would stop.
+enum : uint8_t { STL_SOLID, STL_ENDSOLID, STL_FACET, STL_ENDFACET, STL_LOOP, STL_ENDLOOP, STL_VERTEX, STL_BADVERTEX };
+
+struct StlPart {
+    std::vector<uint8_t> ev;   // one event per keyword line
+    std::vector<float> xyz;    // the numbers of its STL_VERTEX events, in order
+};
+
+void parse_stl_chunk(const char *b, const char *e, StlPart &out)
 {
-    bool in_solid = false, in_facet = false, in_loop = false;
-    int in_facet_n = 0;
-    uint32_t start = 0;
-    const char *b = buf.data(), *e = b + buf.size();
     for (const char *ls = b; ls < e;) {
         const char *le = static_cast<const char *>(memchr(ls, '\n', (size_t)(e - ls)));
         if (!le) le = e;
         const char *p = ls;
         while (p < le && is_ws(*p)) ++p;
         if (p < le) {
-            if (starts_ci(p, le, "solid")) in_solid = true;
-            else if (starts_ci(p, le, "endsolid")) in_solid = false;
-            else if (starts_ci(p, le, "facet")) {
+            if (starts_ci(p, le, "solid")) out.ev.push_back(STL_SOLID);
+            else if (starts_ci(p, le, "endsolid")) out.ev.push_back(STL_ENDSOLID);
+            else if (starts_ci(p, le, "facet")) out.ev.push_back(STL_FACET);
+            else if (starts_ci(p, le, "endfacet")) out.ev.push_back(STL_ENDFACET);
+            else if (starts_ci(p, le, "outer loop")) out.ev.push_back(STL_LOOP);
+            else if (starts_ci(p, le, "endloop")) out.ev.push_back(STL_ENDLOOP);
+            else if (starts_ci(p, le, "vertex")) {
+                const char *q = p;
+                while (q < le && !is_ws(*q)) ++q;   // the keyword token
+                float x, y, z;
+                if (parse_float(q, le, x) && parse_float(q, le, y) && parse_float(q, le, z)) {
+                    out.ev.push_back(STL_VERTEX);
+                    out.xyz.push_back(x);
+                    out.xyz.push_back(y);
+                    out.xyz.push_back(z);
+                } else {
+                    out.ev.push_back(STL_BADVERTEX);
+                }
+            }
+        }
+        ls = le + 1;
+    }
+}
+
+int load_ascii_stl(const std::vector<char> &buf, sdfgen_mesh &m, char *errbuf, size_t errlen)
+{
+    const int T = n_threads(buf.size());
+    const std::vector<size_t> cut = split_lines(buf, T);
+    std::vector<StlPart> part(T);
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] { parse_stl_chunk(buf.data() + cut[t], buf.data() + cut[t + 1], part[t]); });
+    for (auto &x : th) x.join();
+    size_t nv = 0;
+    for (auto &p : part) nv += p.xyz.size();
+    m.xyz.reserve(nv);
+    bool in_solid = false, in_facet = false, in_loop = false;
+    int in_facet_n = 0;
+    uint32_t start = 0;
+    for (auto &p : part) {
+        size_t vi = 0;
+        for (const uint8_t ev : p.ev) {
+            switch (ev) {
+            case STL_SOLID: in_solid = true; break;
+            case STL_ENDSOLID: in_solid = false; break;
+            case STL_FACET:
                 if (!in_solid) return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "'facet' outside 'solid' block");
                 in_facet = true;
                 in_facet_n = 0;
                 start = (uint32_t)(m.xyz.size() / 3);
-            } else if (starts_ci(p, le, "endfacet")) {
+                break;
+            case STL_ENDFACET:
                 if (in_facet_n != 3)
                     return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "Facet has %d vertices (expected 3)", in_facet_n);
                 in_facet = false;
                 m.tri.push_back(start);
                 m.tri.push_back(start + 1);
                 m.tri.push_back(start + 2);
-            } else if (starts_ci(p, le, "outer loop")) in_loop = true;
-            else if (starts_ci(p, le, "endloop")) in_loop = false;
-            else if (starts_ci(p, le, "vertex")) {
+                break;
+            case STL_LOOP: in_loop = true; break;
+            case STL_ENDLOOP: in_loop = false; break;
+            default:   // STL_VERTEX, STL_BADVERTEX
                 if (!in_facet || !in_loop) return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "'vertex' outside facet/loop");
-                const char *q = p;
-                while (q < le && !is_ws(*q)) ++q;   // the keyword token
-                float x, y, z;
-                if (!(parse_float(q, le, x) && parse_float(q, le, y) && parse_float(q, le, z)))
-                    return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "Failed to parse vertex");
-                m.xyz.push_back(x);
-                m.xyz.push_back(y);
-                m.xyz.push_back(z);
+                if (ev == STL_BADVERTEX) return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "Failed to parse vertex");
+                m.xyz.insert(m.xyz.end(), p.xyz.begin() + vi, p.xyz.begin() + vi + 3);
+                vi += 3;
                 ++in_facet_n;
+                break;
             }
         }
-        ls = le + 1;
     }
     if (m.xyz.empty()) return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "No vertices found in ASCII STL file");
     if (m.tri.empty()) return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "No faces found in ASCII STL file");

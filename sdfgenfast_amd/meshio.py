@@ -37,11 +37,23 @@ _libc.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
 
 
 def _parse_f32(tok: str) -> np.float32:
-    # C++ `istream >> float` is strtof-correct rounding; float(tok) then a cast
-    # to float32 would double-round.
+    """`istream >> float` on one token: strtof's correct rounding (float(tok) then a cast to
+    float32 would double-round); ValueError where the stream would fail -- nothing numeric,
+    inf / nan (num_get does not read them) or an overflow; "0x..." reads as 0 (num_get stops
+    at the 'x')."""
+    t = tok.lstrip("+") if tok.startswith("+") and not tok.startswith("+-") else tok
+    low = t.lstrip("-").lower()
+    if low.startswith(("inf", "nan")):
+        raise ValueError(f"not a number: {tok!r}")
+    if low.startswith("0x"):
+        return np.float32(-0.0) if t.startswith("-") else np.float32(0.0)
+    b = t.encode()
+    buf = ctypes.create_string_buffer(b)
     end = ctypes.c_char_p()
-    b = tok.encode()
-    v = _libc.strtof(b, ctypes.byref(end))
+    v = _libc.strtof(buf, ctypes.byref(end))
+    used = ctypes.cast(end, ctypes.c_void_p).value - ctypes.addressof(buf)
+    if used <= 0 or not np.isfinite(v):
+        raise ValueError(f"not a number: {tok!r}")
     return np.float32(v)
 
 
@@ -141,7 +153,10 @@ def _load_obj(path: str):
                 tok = line.split()
                 if len(tok) < 4:
                     continue
-                verts.append([_parse_f32(t) for t in tok[1:4]])
+                try:
+                    verts.append([_parse_f32(t) for t in tok[1:4]])
+                except ValueError:
+                    continue   # mesh_io_obj.cpp:77-80: warn and skip the line
             elif line[0] == "f" and len(line) > 1 and line[1] in " \t":
                 idx = [int(t.split("/")[0]) for t in line.split()[1:]]
                 if len(idx) < 3:
