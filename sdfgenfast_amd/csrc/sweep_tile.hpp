@@ -71,6 +71,12 @@ namespace sdfhip {
 #ifndef ST_TWIN
 #define ST_TWIN 1      // twin lanes split each cell's candidates (needs 32-cell compute waves)
 #endif
+#ifndef ST_HSLEEP
+#define ST_HSLEEP 16   // longest back-off (s_sleep units of 64 cycles) of an idle helper wave
+#endif
+#ifndef ST_CSLEEP
+#define ST_CSLEEP 8    // longest back-off of a waiting compute wave
+#endif
 #ifndef ST_WPE_DEF
 #define ST_WPE_DEF 3   // waves per SIMD the register budget must allow
 #endif
@@ -477,7 +483,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     // waiting tiles back off: their polls share the SIMD with the tiles they wait for
                     if (polls < 8) __builtin_amdgcn_s_sleep(1);
                     else if (polls < 64) __builtin_amdgcn_s_sleep(2);
-                    else __builtin_amdgcn_s_sleep(8);
+                    else __builtin_amdgcn_s_sleep(ST_CSLEEP);
                 }
                 __builtin_amdgcn_s_setprio(ST_WORK_PRIO);
                 asm volatile("" ::: "memory");   // no LDS read moves above the readiness poll
@@ -794,7 +800,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         }
                         if (idle < 4) __builtin_amdgcn_s_sleep(1);
                         else if (idle < 16) __builtin_amdgcn_s_sleep(4);
-                        else __builtin_amdgcn_s_sleep(16);
+                        else __builtin_amdgcn_s_sleep(ST_HSLEEP);
                         continue;
                     }
                 }
@@ -900,7 +906,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                     if (idle < 4) __builtin_amdgcn_s_sleep(1);
                     else if (idle < 16) __builtin_amdgcn_s_sleep(4);
-                    else __builtin_amdgcn_s_sleep(16);
+                    else __builtin_amdgcn_s_sleep(ST_HSLEEP);
                 }
             }
         }
