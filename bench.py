@@ -182,6 +182,7 @@ def measure_zslab(workload, steps, warmup, dev, dist, world, rank, verify=True):
     sess = D._gpu_session(dist, None, dev, dims, world, rank)
     out = _hiprt.DeviceBuffer(ni * nj * (sess.k_end - sess.k_begin) * 4)
     sess.prepare(t.shape[0])
+    dist.barrier()   # every slab's buffers and tables are in place before any slab's kernels wait on it
 
     def step():
         sess.enqueue(dt.ptr, t.shape[0], dv.ptr, v.shape[0], o, dx, 1, _lib.LAYOUT_ARRAY3, out.ptr)
