@@ -6,8 +6,11 @@ this module.  The product package (sdfgenfast_amd) never does.
 * ``liboracle.so``  -- oracle/sdf_oracle.c, the C restatement of
   cpu_lib/makelevelset3.cpp:192-304 (single-thread semantics).
 * ``_ref/libsdfref.so`` -- the reference's own cpu_lib/makelevelset3.cpp
-  compiled from /root/reference (development container only; absent on the
-  GPU box).
+  compiled from /root/reference by ``make -C oracle ref`` (``__graft_entry__.build``
+  runs it where /root/reference exists).  The built library is git-ignored but
+  travels with the working tree to the GPU box, where bench.py times it as the
+  CPU baseline (kind "reference"); without it the baseline is the library's own
+  native CPU backend on the same full workload (kind "port").
 """
 from __future__ import annotations
 
