@@ -171,9 +171,11 @@ __device__ __forceinline__ bool sp_in(const SpParams &P, int i, int j, int k)
 // if u's label has not changed since (the sweep stamped in u's low word is <= s'), c has
 // already seen that label.  A label set in this very sweep carries this sweep's stamp,
 // so the LIVE (repair) evaluation needs no extra check.
+// the low words (label, stamp) of the 7 upwind neighbours: half the bytes of the 8-byte cells (a
+// 32-bit load of a 64-bit atomically stored word sees one of its stored values' halves)
 template <bool LIVE, bool SLAB = false>
-__device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned long long *L, int i, int j, int k,
-                                            size_t c, unsigned long long own, int (&lab)[7])
+__device__ __forceinline__ void sp_nb_words(const SpParams &P, const unsigned long long *L, int i, int j, int k,
+                                            size_t c, uint32_t (&w)[7])
 {
     const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
     const long long cc = (long long)c;
@@ -182,22 +184,28 @@ __device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned lo
     const bool halo = SLAB && (k - P.dk < P.k_lo || k - P.dk >= P.k_hi);
     const long long hp = (long long)i + (long long)P.ni * j;   // plane index of (i, j)
     const long long hnb[3] = {hp, hp - P.di, hp - (long long)P.dj * P.ni};   // q = 3 (k), 4 (i,k), 5 (j,k); 6 below
-    int lcq[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
-        // the low word (label, stamp) only: half the bytes of the 8-byte cell (a 32-bit load of
-        // a 64-bit atomically stored word sees one of its stored values' halves)
-        uint32_t w;
         if (SLAB && q >= 3 && halo) {
             const long long hq = q == 6 ? hp - P.di - (long long)P.dj * P.ni : hnb[q - 3];
             const uint32_t *hw = (LIVE ? P.hX_up : P.hS_up) + SDF_CHK(23, hq, 0, (size_t)P.ni * P.nj);
-            w = __hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            w[q] = __hip_atomic_load(hw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
             const uint32_t *lw = reinterpret_cast<const uint32_t *>(L + SDF_CHK(22, nb[q], P.c_lo, P.c_lo + P.n));
-            w = LIVE ? sp_ld32(lw) : *lw;
+            w[q] = LIVE ? sp_ld32(lw) : *lw;
         }
-        lab[q] = lbl_of(w);
-        lcq[q] = lc_of(w);
+    }
+}
+
+// the candidate mask from the neighbours' low words
+__device__ __forceinline__ unsigned sp_mask_w(const SpParams &P, int i, int j, int k, unsigned long long own,
+                                              const uint32_t (&w)[7], int (&lab)[7], bool live)
+{
+    int lcq[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        lab[q] = lbl_of(w[q]);
+        lcq[q] = lc_of(w[q]);
     }
     const int ct0 = lbl_of((uint32_t)own);
     const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
@@ -212,17 +220,27 @@ __device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned lo
         f |= (skip ? 0u : 1u) << q;
     }
 #ifdef SP_JACOBI_NOEVAL   // diagnostics only: the Jacobi pass's memory floor (wrong results)
-    if (!LIVE) f = 0;
+    if (!live) f = 0;
 #endif
     return f;
 }
 
 template <bool LIVE, bool SLAB = false>
-__device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
-                                                      int k, size_t c, unsigned long long own)
+__device__ __forceinline__ unsigned sp_mask(const SpParams &P, const unsigned long long *L, int i, int j, int k,
+                                            size_t c, unsigned long long own, int (&lab)[7])
+{
+    uint32_t w[7];
+    sp_nb_words<LIVE, SLAB>(P, L, i, j, k, c, w);
+    return sp_mask_w(P, i, j, k, own, w, lab, LIVE);
+}
+
+// f(own, upwind labels) from the neighbours' low words
+template <bool LIVE>
+__device__ __forceinline__ unsigned long long sp_eval_w(const SpParams &P, int i, int j, int k,
+                                                        unsigned long long own, const uint32_t (&w)[7])
 {
     int lab[7];
-    unsigned f = sp_mask<LIVE, SLAB>(P, L, i, j, k, c, own, lab);
+    unsigned f = sp_mask_w(P, i, j, k, own, w, lab, LIVE);
     float phi = __uint_as_float((uint32_t)(own >> 32));
     int ct = lbl_of((uint32_t)own);
     bool changed = false;
@@ -277,6 +295,15 @@ __device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const u
 #endif
     if (!changed) return own;
     return ((unsigned long long)__float_as_uint(phi) << 32) | lo_word(ct, P.sweep + 1);
+}
+
+template <bool LIVE, bool SLAB = false>
+__device__ __forceinline__ unsigned long long sp_eval(const SpParams &P, const unsigned long long *L, int i, int j,
+                                                      int k, size_t c, unsigned long long own)
+{
+    uint32_t w[7];
+    sp_nb_words<LIVE, SLAB>(P, L, i, j, k, c, w);
+    return sp_eval_w<LIVE>(P, i, j, k, own, w);
 }
 
 

@@ -3,15 +3,21 @@ import json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 wl, cfgs = sys.argv[1], sys.argv[2:]
 code = r'''
-import sys, json; sys.path.insert(0, %r)
+import sys, json, os, hashlib; sys.path.insert(0, %r)
+import numpy as np
 from sdfgenfast_amd import _lib, meshgen
-v, t, o, dx, dims = meshgen.workload(%r)
+wl = %r
+v, t, o, dx, dims = meshgen.workload(wl)
+ref = json.load(open(os.path.join(sys.path[0], "tests", "golden", "hashes.json"))).get(wl, {}).get("sha256_phi")
 best = None
 for rep in range(6):
-    _lib.make_level_set3(v, t, o, dx, *dims, 1)
+    phi = _lib.make_level_set3(v, t, o, dx, *dims, 1)
+    if rep == 0 and ref:
+        got = hashlib.sha256(np.asfortranarray(phi).ravel(order="F").astype("<f4").tobytes()).hexdigest()
+        digest = "ok" if got == ref else "MISMATCH"
     p = _lib.last_profile()
     if rep and (best is None or p["total_ms"] < best["total_ms"]): best = p
-print(json.dumps({k: best[k] for k in ("total_ms", "band_ms", "sweep_ms")} | {"sw": [round(x, 3) for x in best["sweep_launch_ms"]]}))
+print(json.dumps({k: best[k] for k in ("total_ms", "band_ms", "sweep_ms")} | {"sw": [round(x, 3) for x in best["sweep_launch_ms"]], "digest": digest if ref else "-"}))
 ''' % (ROOT, wl)
 for rnd in range(2):
     for cfg in cfgs:
@@ -24,4 +30,4 @@ for rnd in range(2):
         if r.returncode:
             print(cfg, "FAILED", r.stderr[-800:]); sys.exit(1)
         d = json.loads(r.stdout.strip().splitlines()[-1])
-        print(f"{cfg:28s} total {d['total_ms']:7.3f} band {d['band_ms']:6.3f} sweep {d['sweep_ms']:7.3f} | tile {sum(d['sw'][:8]):6.3f} sparse {sum(d['sw'][8:]):6.3f}", flush=True)
+        print(f"{cfg:28s} total {d['total_ms']:7.3f} band {d['band_ms']:6.3f} sweep {d['sweep_ms']:7.3f} | tile {sum(d['sw'][:8]):6.3f} sparse {sum(d['sw'][8:]):6.3f} digest {d['digest']}", flush=True)
