@@ -862,6 +862,9 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 n2 = n3 = ~0ull;
                 m2 = m3 = 0ull;
 #endif
+#ifdef ST_HALO_DELAY   // diagnostics: the first pass's sensitivity to the tile-hop latency
+                if (__any(hp > 0)) __builtin_amdgcn_s_sleep(ST_HALO_DELAY);
+#endif
                 // ---- land batch A in LDS, then publish readiness ----
 #define ST_LAND(g, cg, qg)                                                                             \
     if (ST_OWN_OK(g)) {                                                                                \
