@@ -87,6 +87,9 @@ inline unsigned sp_shards(unsigned long long n)
     return q;
 }
 constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup 0's lanes)
+#ifndef SP_SPLIT_APPEND
+#define SP_SPLIT_APPEND 1   // k_sp_recheck: the append's atomic overlaps the next iteration's first round trip
+#endif
 #ifndef SP_IDLE_SLEEP
 #define SP_IDLE_SLEEP 2
 #endif
@@ -376,6 +379,57 @@ __device__ __forceinline__ void sp_append_wave(const SpParams &P, unsigned shard
         if ((qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + (t++) % P.cap, (unsigned)(tgt[q] + 1));
 }
 
+// sp_append_wave in two halves, so that the append's round trip overlaps the next iteration's
+// first one (k_sp_recheck, SP_SPLIT_APPEND): sp_append_issue makes the wave's ONE atomic on the
+// shard word (inline asm: the compiler's atomic optimiser would wait for it on the spot) and keeps
+// what the stores need; sp_append_finish waits for the returned tail and stores the cells.  Until
+// then the slots read 0 (a poller retries), while the items already count as pending.
+struct SpAppend {
+    unsigned long long old_q;   // lane 0: the shard word before the atomic (in flight until finish)
+    unsigned long long tot;     // items appended by the wave
+    unsigned pre;               // this lane's first item's offset
+    unsigned qmask;             // this lane's items (slots of tgt)
+    bool live;                  // wave-uniform: an atomic is in flight
+};
+__device__ __forceinline__ void sp_append_issue(const SpParams &P, unsigned shard, unsigned qmask, bool fin, SpAppend &A)
+{
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned nq = __popc(qmask);
+    const unsigned long long b0 = __ballot(nq & 1u), b1 = __ballot(nq & 2u), b2 = __ballot(nq & 4u),
+                             bf = __ballot(fin);
+    A.live = (b0 | b1 | b2 | bf) != 0ull;
+    if (!A.live) return;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    A.pre = (unsigned)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+    A.tot = (unsigned long long)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    A.qmask = qmask;
+    const unsigned long long nfin = (unsigned long long)__popcll(bf);
+    if (lane == 0) {
+        // pending += tot - nfin, tail += tot (two's complement in the high half)
+        unsigned long long *w = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];
+        const unsigned long long d = (A.tot - nfin) * SP_PENDING_ONE + A.tot;
+        // (s_nop 1: hipcc pads nothing inside asm -- the operand registers are rewritten right after)
+        asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_nop 1" : "=&v"(A.old_q) : "v"(w), "v"(d) : "memory");
+    }
+}
+__device__ __forceinline__ void sp_append_finish(const SpParams &P, unsigned shard, const size_t (&tgt)[7], SpAppend &A)
+{
+    if (!A.live) return;
+    A.live = false;
+    const unsigned lane = threadIdx.x & 63;
+    unsigned long long t0 = 0;
+    if (lane == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(A.old_q)::"memory");   // the returned word has landed
+        t0 = A.old_q & 0xffffffffull;
+        if (t0 + A.tot > SP_TAIL_LIMIT) atomicOr(&P.ctl[SP_ERR], 2ull);
+    }
+    t0 = ((unsigned long long)(unsigned)__shfl((int)(t0 >> 32), 0) << 32) | (unsigned)__shfl((int)t0, 0);
+    unsigned long long t = t0 + A.pre;
+#pragma unroll
+    for (int q = 0; q < 7; ++q)
+        if ((A.qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + (t++) % P.cap, (unsigned)(tgt[q] + 1));
+}
+
 // Pass 1 of the sparse sweep: every cell against the labels of S, in two kernels.
 // k_sp_jacobi streams the grid: a cell with no label left to examine (sp_mask == 0,
 // ~90 % of them) is copied to X as is; the others are appended to a compact list that
@@ -555,6 +609,11 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
     unsigned long long *const q_tail = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];   // pending << 32 | tail
     unsigned long long *const q_head = q_tail + 16;
     unsigned *const ring = P.queue + (size_t)shard * P.cap;
+#if SP_SPLIT_APPEND
+    SpAppend app;
+    app.live = false;
+    size_t tgt_app[7];   // the cells of the append in flight
+#endif
     for (;;) {
         unsigned qmask = 0;   // cells this lane queues this iteration (sp_append_wave below)
         size_t tgt[7];
@@ -579,6 +638,9 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             if (lane == 0) qw = sp_ld64(q_tail);
             qw = ((unsigned long long)(unsigned)__shfl((int)(qw >> 32), 0) << 32) | (unsigned)__shfl((int)qw, 0);
         }
+#if SP_SPLIT_APPEND
+        sp_append_finish(P, shard, tgt_app, app);   // last iteration's append (its atomic overlapped the above)
+#endif
         if (SLAB && in_role && e == NONE) {
             if (!in_wait) {
                 h_in = atomicAdd(&P.ctl[SP_INHEAD], 1ull);
@@ -662,8 +724,20 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 sp_order();
             }
         }
+#if SP_SPLIT_APPEND
+        sp_append_issue(P, shard, qmask, fin, app);
+        if (app.live) {
+#pragma unroll
+            for (int q = 0; q < 7; ++q) tgt_app[q] = tgt[q];
+        }
+        if (__all(done)) {
+            sp_append_finish(P, shard, tgt_app, app);
+            break;
+        }
+#else
         sp_append_wave(P, shard, qmask, tgt, fin);
         if (__all(done)) break;
+#endif
         if (SP_IDLE_SLEEP && !__any(e != NONE)) __builtin_amdgcn_s_sleep(SP_IDLE_SLEEP);
     }
     if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
