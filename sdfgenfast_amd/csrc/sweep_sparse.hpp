@@ -336,10 +336,11 @@ __device__ __forceinline__ size_t sp_request_collect(const SpParams &P, int i, i
         const bool ui = m & 1, uj = m & 2, uk = m & 4;
         const bool ok = !((ui && !ii) || (uj && !jj) || (uk && !kk) || (!uk && !k0));
         tgt[q] = ok ? (size_t)(cc + (ui ? si : 0) + (uj ? sj : 0) + (uk ? sk : 0)) : ~(size_t)0;
-        // branch-free: a slot with no target adds 0 to this cell's own counter.  (A conditional
+        // branch-free: a slot with no target adds 0 to the range's first counter (not to c's own:
+        // an inbound entry's c is the upstream slab's cell, outside this range).  (A conditional
         // atomic merged with a constant made hipcc wait for each of the 7 in turn: 7 round trips.)
 #if SP_REQ_BRANCHFREE
-        const unsigned r = atomicAdd(&P.req[SDF_CHK(24, ok ? tgt[q] : c, P.c_lo, P.c_lo + P.n)], ok ? 1u : 0u);
+        const unsigned r = atomicAdd(&P.req[SDF_CHK(24, ok ? tgt[q] : (size_t)P.c_lo, P.c_lo, P.c_lo + P.n)], ok ? 1u : 0u);
         old[q] = ok ? r : 1u;
 #else
         old[q] = ok ? atomicAdd(&P.req[SDF_CHK(24, tgt[q], P.c_lo, P.c_lo + P.n)], 1u) : 1u;
