@@ -766,7 +766,11 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             // address; lanes off the tile's edge read the tile's first column (a Z-slab holds only
             // its own planes: (0, 0, 0) may lie in another GPU's slab).  (b0, c0: the tile's corner,
             // before the batch registers below shadow the name c0.)
+#ifdef ST_TDUMMY   // experiment: every unused slot of the tile reads ONE line (coalesced per wave)
+            const size_t dummy = st_phys(P, 0, b0, c0);
+#else
             const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, b0, c0);
+#endif
             int fA = 0, gA = 0;                    // own steps [fA, fA+gA) whose cells are in c0..c3
             int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
