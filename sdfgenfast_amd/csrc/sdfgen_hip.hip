@@ -289,11 +289,7 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
                 if (key == ~0ull) continue;
                 const unsigned ij = (unsigned)(uni * unj), kk = c / ij, rem = c - kk * ij, jj = rem / (unsigned)uni;
                 u64 *p = cell + cidx(ui0 + (int)(rem - jj * (unsigned)uni), uj0 + (int)jj, uk0 + (int)kk, g.ni, g.nj);
-#ifdef BAND_NOCHECK
-                atomicMin(p, key);
-#else
-                if (key < *p) atomicMin(p, key);
-#endif
+                atomicMin(p, key);   // no load-compare first: 0.81 -> 0.78 ms at C3 (no return to wait for)
             }
         __syncthreads();
     }

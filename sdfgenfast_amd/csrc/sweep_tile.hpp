@@ -762,15 +762,19 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             // All loads are unconditional (invalid slots read a clamped address and are
             // ignored), so hipcc's waitcnt pass can count them and waits for the stage-2
             // gathers only, leaving the younger stage-1 loads in flight.
-            // unused load slots read this lane's own column start (spread, cached), never one hot
-            // address; lanes off the tile's edge read the tile's first column (a Z-slab holds only
-            // its own planes: (0, 0, 0) may lie in another GPU's slab).  (b0, c0: the tile's corner,
+            // unused load slots read the tile's first column start: one cached line per tile, so
+            // not one hot address for the chip, and inside the slab (a Z-slab holds only its own
+            // planes: (0, 0, 0) may lie in another GPU's slab).  (b0, c0: the tile's corner,
             // before the batch registers below shadow the name c0.)
-#ifdef ST_TDUMMY   // experiment: every unused slot of the tile reads ONE line (coalesced per wave)
+            // (one line for the whole wave: a per-lane dummy -- each lane its own column start, 47
+            // non-halo lanes' granule slots among them -- cost every load instruction up to 64 line
+            // requests; one shared line took the first pass 14.2 -> 13.9 ms at 256^3, 53.9 -> 51.6
+            // ms at 512^3)
             const size_t dummy = st_phys(P, 0, b0, c0);
-#else
-            const size_t dummy = col ? st_phys(P, 0, b, c) : st_phys(P, 0, b0, c0);
-#endif
+            // gathers with nothing to fetch read a per-tile triangle: triangle 0 for every tile was one
+            // hot line for the whole chip (first pass 14.0 -> 13.9 ms at 256^3, 51.4 -> 50.6 ms at 512^3)
+            // (0 when the triangle count is unknown: ntri is ~0 until a pipeline sets it)
+            const int gdum = (P.ntri >= 1 && P.ntri < 0x7fffffffull) ? (int)((unsigned)(J * 40503 + K * 9973 + 17) % (unsigned)P.ntri) : 0;
             int fA = 0, gA = 0;                    // own steps [fA, fA+gA) whose cells are in c0..c3
             int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
@@ -822,12 +826,21 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
 #define ST_GATHER(g, cg, qg)                                                                          \
-    const size_t so##g = 3 * SDF_CHK(11, (ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : 0), 0, P.ntri); \
+    const size_t so##g = 3 * SDF_CHK(11, (ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
     const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
-    const size_t sh##g = 3 * SDF_CHK(12, ((g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : 0), 0, P.ntri); \
+    const size_t sh##g = 3 * SDF_CHK(12, ((g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
     const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
                 ST_GATHER(0, c0, q0)
+#ifdef ST_OWNDEDUP   // experiment: slot 1 repeating slot 0's label reads the shared dummy line instead
+                const bool dup1 = ST_OWN_OK(0) && ST_OWN_OK(1) && lbl_of((uint32_t)c1) == lbl_of((uint32_t)c0);
+                const bool hdup1 = 0 < hp && 1 < hp && lbl_of((uint32_t)q1) == lbl_of((uint32_t)q0);
+                const size_t so1 = 3 * SDF_CHK(11, (ST_OWN_OK(1) && !dup1 && lbl_of((uint32_t)c1) >= 0 ? lbl_of((uint32_t)c1) : gdum), 0, P.ntri);
+                const float4 oa1_ = P.soup[so1], ob1_ = P.soup[so1 + 1], oc1_ = P.soup[so1 + 2];
+                const size_t sh1 = 3 * SDF_CHK(12, (1 < hp && !hdup1 && lbl_of((uint32_t)q1) >= 0 ? lbl_of((uint32_t)q1) : gdum), 0, P.ntri);
+                const float4 ha1_ = P.soup[sh1], hb1_ = P.soup[sh1 + 1], hc1_ = P.soup[sh1 + 2];
+#else
                 ST_GATHER(1, c1, q1)
+#endif
 #if ST_G_DEF > 2
                 ST_GATHER(2, c2, q2)
                 ST_GATHER(3, c3, q3)
@@ -884,7 +897,15 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
         s_ent[3 * e_ + 2] = hc##g;                                                                     \
     }
                 ST_LAND(0, c0, q0)
+#ifdef ST_OWNDEDUP
+                {
+                    const float4 oa1 = dup1 ? oa0 : oa1_, ob1 = dup1 ? ob0 : ob1_, oc1 = dup1 ? oc0 : oc1_;
+                    const float4 ha1 = hdup1 ? ha0 : ha1_, hb1 = hdup1 ? hb0 : hb1_, hc1 = hdup1 ? hc0 : hc1_;
+                    ST_LAND(1, c1, q1)
+                }
+#else
                 ST_LAND(1, c1, q1)
+#endif
 #if ST_G_DEF > 2
                 ST_LAND(2, c2, q2)
                 ST_LAND(3, c3, q3)
