@@ -6,7 +6,8 @@ cd "$(dirname "$0")/.."
 mkdir -p ab/build_$1
 H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -fno-slp-vectorize -Iinclude -Isdfgenfast_amd/csrc $2"
-$H --offload-arch=gfx950 $F -c sdfgenfast_amd/csrc/sdfgen_hip.hip -o ab/build_$1/a.o
+D="${DEVFLAGS--mllvm -amdgpu-sched-strategy=iterative-ilp}"   # the Makefile's device code generation flags
+$H --offload-arch=gfx950 $F $D -c sdfgenfast_amd/csrc/sdfgen_hip.hip -o ab/build_$1/a.o
 $H -x hip --offload-arch=gfx950 $F -c sdfgenfast_amd/csrc/cpu_backend.cpp -o ab/build_$1/b.o
 $H $F -c sdfgenfast_amd/csrc/sdfgen_unified.cpp -o ab/build_$1/c.o
 $H $F -c sdfgenfast_amd/csrc/meshio.cpp -o ab/build_$1/d.o
