@@ -252,8 +252,11 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
     // per compute wave: (entry << 9 | q << 6 | lane) list, then one trash word per lane (the
     // target of lanes with nothing to store, so the stores need no divergent branch)
-    __shared__ int s_pair[ST_NCW][7 * ST_CPW + 64];
-    __shared__ float s_d[ST_NCW][7 * ST_CPW + 64];   // per compute wave: distance of candidate q for lane
+    // s_pd[w]: [0, 7 CPW) the (entry << 9 | q << 6 | lane) list, [7 CPW, 14 CPW) the distance bits of
+    // candidate q for lane (q * CPW + lane), then ONE trash word per lane shared by both (the target of
+    // lanes with nothing to store, so the stores need no divergent branch; one trash area instead of
+    // two leaves room for a 16-slot halo ring at 3 tiles per CU)
+    __shared__ int s_pd[ST_NCW][14 * ST_CPW + 64];
     // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
     // compute wave w.
     __shared__ __attribute__((aligned(16))) int s_hdr[4];
@@ -629,18 +632,18 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     const unsigned long long m = __ballot(f);
                     const int pos = total + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    s_pair[w][f ? pos : 7 * ST_CPW + L] = (ent[q] << 9) | (q << 6) | L;
+                    s_pd[w][f ? pos : 14 * ST_CPW + L] = (ent[q] << 9) | (q << 6) | L;
                     total += (int)__popcll(m);
                 }
                 // ---- evaluate (<= 112 pairs): one per lane, a second chain only if needed ----
                 for (int k = L; k < total; k += 128) {
-                    const int p1 = s_pair[w][k];
+                    const int p1 = s_pd[w][k];
                     const bool has2 = k + 64 < total;
                     const int l1 = p1 & 63, e1 = p1 >> 9;
                     const f3 g1 = st_gx(P, h - (l1 & 7) - (ST_CLW * w + (l1 >> 3)), b0 + (l1 & 7),
                                         c0 + ST_CLW * w + (l1 >> 3));
                     if (__any(has2)) {
-                        const int p2 = has2 ? s_pair[w][k + 64] : p1;
+                        const int p2 = has2 ? s_pd[w][k + 64] : p1;
                         const int l2 = p2 & 63, e2 = p2 >> 9;
                         const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
                                             c0 + ST_CLW * w + (l2 >> 3));
@@ -648,12 +651,12 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         const float4 v13 = s_ent[__umul24(e1, 3) + 2], v23 = s_ent[__umul24(e2, 3) + 2];
                         ptd_wave2(g1, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v13), v13.w, g2,
                                   st_xyz(s_ent[__umul24(e2, 3)]), st_xyz(s_ent[__umul24(e2, 3) + 1]), st_xyz(v23), v23.w, d1, d2);
-                        s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] = d1;
-                        s_d[w][has2 ? ((p2 >> 6) & 7) * ST_CPW + l2 : 7 * ST_CPW + L] = d2;
+                        s_pd[w][7 * ST_CPW + ((p1 >> 6) & 7) * ST_CPW + l1] = __float_as_int(d1);
+                        s_pd[w][7 * ST_CPW + (has2 ? ((p2 >> 6) & 7) * ST_CPW + l2 : 7 * ST_CPW + L)] = __float_as_int(d2);
                     } else {
-                        s_d[w][((p1 >> 6) & 7) * ST_CPW + l1] =
+                        s_pd[w][7 * ST_CPW + ((p1 >> 6) & 7) * ST_CPW + l1] = __float_as_int(
                             ptd_wave(g1, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(s_ent[__umul24(e1, 3) + 2]),
-                                     s_ent[__umul24(e1, 3) + 2].w);
+                                     s_ent[__umul24(e1, 3) + 2].w));
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
@@ -664,7 +667,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                 if (act) {   // branch-free: all 7 slots read at once, non-candidates masked out
                     float dq[7];
 #pragma unroll
-                    for (int q = 0; q < 7; ++q) dq[q] = s_d[w][q * ST_CPW + L];
+                    for (int q = 0; q < 7; ++q) dq[q] = __int_as_float(s_pd[w][7 * ST_CPW + q * ST_CPW + L]);
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         const bool take = ((fmask >> q) & 1u) && dq[q] < phi;
