@@ -15,11 +15,33 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 // The same functions serve the device kernels and the library's native CPU backend
 // (cpu_backend.cpp, host code of the same hipcc build): SDF_HD marks them for both.
 #define SDF_HD __host__ __device__ __forceinline__
 
 namespace sdfhip {
+
+#if defined(__HIPCC__)
+// Zeroing of small per-call control words as a compute kernel: hipMemsetAsync runs as a runtime
+// blit whose hand-over to the next compute kernel left a ~6 us gap in the stream (kernel trace:
+// one before every second-pass sweep).  A template, so each translation unit may instantiate it.
+template <int = 0>
+__global__ void k_zero32(uint32_t *__restrict__ p, size_t n)
+{
+    for (size_t x = blockIdx.x * (size_t)blockDim.x + threadIdx.x; x < n; x += (size_t)gridDim.x * blockDim.x) p[x] = 0u;
+}
+// bytes: a multiple of 4
+inline hipError_t zero_async(void *p, size_t bytes, hipStream_t st)
+{
+    const size_t n = bytes / 4;
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(k_zero32<>, dim3(blocks), dim3(256), 0, st, (uint32_t *)p, n);
+    return hipGetLastError();
+}
+#endif
 
 // IEEE correctly-rounded float sqrt and division on both sides.  NOTE: on ROCm 7.2
 // __fsqrt_rn() lowers to a bare v_sqrt_f32 (1 ulp, NOT correctly rounded); the

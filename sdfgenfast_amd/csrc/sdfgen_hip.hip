@@ -438,6 +438,24 @@ __global__ void k_debug_pit2d(uint64_t n, const double *__restrict__ in, double 
 const int SWEEP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
                               {+1, -1, +1}, {-1, +1, -1}, {+1, -1, -1}, {-1, +1, +1}};
 
+// Status words of one call (run_pipeline): [0] prep error flag, [1] tile sweep error bits, [2] band
+// evaluations, [3, 19) tile sweep statistics, [19, 19 + SP_NCTL) the sparse sweeps' control words.
+constexpr int STATUS_N = 19 + SP_NCTL;
+__global__ void k_status(unsigned long long *__restrict__ out, const int *flag, const int *wf_err,
+                         const unsigned long long *evals, const unsigned long long *wf_stats,
+                         const unsigned long long *sp_ctl)
+{
+    for (int t = threadIdx.x; t < STATUS_N; t += blockDim.x) {
+        unsigned long long v = 0;
+        if (t == 0) v = (unsigned)*flag;
+        else if (t == 1) v = wf_err ? (unsigned)*wf_err : 0u;
+        else if (t == 2) v = *evals;
+        else if (t < 19) v = wf_stats ? wf_stats[t - 3] : 0ull;
+        else v = sp_ctl ? sp_ctl[t - 19] : 0ull;
+        out[t] = v;
+    }
+}
+
 struct Workspace {
     int device = -1;
     hipStream_t stream = nullptr;
@@ -448,6 +466,7 @@ struct Workspace {
     float *xyz = nullptr;
     int *err_flag = nullptr;
     unsigned long long *evals = nullptr;
+    unsigned long long *status = nullptr;   // STATUS_N words gathered by k_status, read back in one copy
     size_t cap_cell = 0, cap_cnt = 0, cap_soup = 0, cap_tri = 0, cap_xyz = 0;
     hipEvent_t ev[40] = {};
     bool ev_ok = false;
@@ -550,6 +569,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     if (!ws->err_flag) {
         HIPCHK(hipMalloc((void **)&ws->err_flag, sizeof(int)));
         HIPCHK(hipMalloc((void **)&ws->evals, sizeof(unsigned long long)));
+        HIPCHK(hipMalloc((void **)&ws->status, STATUS_N * sizeof(unsigned long long)));
     }
     Grid g{origin[0], origin[1], origin[2], dx, ni, nj, nk};
     const float init = (float)(ni + nj + nk) * dx;  // :197
@@ -557,8 +577,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
 
     hipEvent_t *ev = ws->ev;
     HIPCHK(hipEventRecord(ev[0], st));
-    HIPCHK(hipMemsetAsync(ws->err_flag, 0, sizeof(int), st));
-    HIPCHK(hipMemsetAsync(ws->evals, 0, sizeof(unsigned long long), st));
+    HIPCHK(zero_async(ws->err_flag, sizeof(int), st));
+    HIPCHK(zero_async(ws->evals, sizeof(unsigned long long), st));
     if (ntri) {
         hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, d_tri, ntri, d_xyz, nvert,
                            ws->soup, ws->err_flag);
@@ -613,8 +633,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     ws->wf.chi = n;
     ws->wf.ntri = ntri;
     ws->sp.ntri = ntri;
-    if (ws->wf.ctrl) HIPCHK(hipMemsetAsync(ws->wf.ctrl + 1, 0, sizeof(int), st));   // error bits of this call
-    if (sparse_first < 16 && ws->sp.ctl) HIPCHK(hipMemsetAsync(ws->sp.ctl, 0, SP_NCTL * sizeof(u64), st));
+    if (ws->wf.ctrl) HIPCHK(zero_async(ws->wf.ctrl + 1, sizeof(int), st));   // error bits of this call
+    if (sparse_first < 16 && ws->sp.ctl) HIPCHK(zero_async(ws->sp.ctl, SP_NCTL * sizeof(u64), st));
     // The first pass's tile sweeps as ONE launch whose sweeps overlap (tile_sweep_multi) unless
     // SDFGEN_TILE_MULTI=0, tracing is on, or the per-sweep halo buffers (17 GB at 1024^3) would
     // take more than half of the free device memory; its time is then reported as sweep 0's
@@ -630,8 +650,17 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         const double have = (double)free_b + (double)ws->wf.cap_mhb * 8.0 + (double)ws->wf.cap_mhc * 8.0;
         if (!(e && atoi(e) == 0) && want > 1 && bytes <= 0.5 * have) multi_n = want;
     }
+    // sweeps 1..multi_n-1 run inside sweep 0's launch: no event of their own (back-to-back event
+    // records cost ~5 us of stream time each: a 37 us gap after the first pass in the kernel trace)
+    // Likewise the second pass's sweeps after the first are timed together (in sweep sparse_first's
+    // slot) unless SDFGEN_SWEEP_EVENTS asks for per-sweep times (diagnostics: ~6 us of stream time
+    // per event between two kernels).
+    static const bool per_sweep_events = getenv("SDFGEN_SWEEP_EVENTS") != nullptr;
+    auto evrec = [&](int s) {
+        return !(multi_n > 1 && s >= 1 && s < multi_n) && (per_sweep_events || s <= sparse_first || s >= nsweeps);
+    };
     for (int s = 0; s < 16; ++s) {
-        HIPCHK(hipEventRecord(ev[3 + s], st));
+        if (evrec(s)) HIPCHK(hipEventRecord(ev[3 + s], st));
         if (!do_sweep || s >= nsweeps) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
         if (impl == 1 && s >= sparse_first) {
@@ -678,17 +707,17 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[20], st));
-    int flag = 0, wf_err = 0;
-    unsigned long long evals = 0, wf_stats[16] = {}, sp_ctl[SP_NCTL] = {};
-    if (sparse_sweeps)
-        HIPCHK(hipMemcpyAsync(sp_ctl, ws->sp.ctl, sizeof(sp_ctl), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    if (impl == 1 && ws->wf.ctrl) {
-        HIPCHK(hipMemcpyAsync(&wf_err, ws->wf.ctrl + 1, sizeof(int), hipMemcpyDeviceToHost, st));
-        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemcpyAsync(wf_stats, ws->wf.stats, sizeof(wf_stats), hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipMemcpyAsync(&evals, ws->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
+    // every status word of the call gathered on the device and read back in ONE copy (four small
+    // copies cost ~70 us at the end of every call: kernel trace)
+    unsigned long long stv[STATUS_N] = {};
+    hipLaunchKernelGGL(k_status, dim3(1), dim3(256), 0, st, ws->status, ws->err_flag,
+                       (impl == 1 && ws->wf.ctrl) ? ws->wf.ctrl + 1 : nullptr, ws->evals,
+                       (impl == 1 && ws->wf.count) ? ws->wf.stats : nullptr, sparse_sweeps ? ws->sp.ctl : nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(stv, ws->status, sizeof(stv), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    const int flag = (int)stv[0], wf_err = (int)stv[1];
+    const unsigned long long evals = stv[2], *wf_stats = stv + 3, *sp_ctl = stv + 19;
     HIPCHK(hipGetLastError());
     if ((rc = check_oob(err, "make_level_set3"))) return rc;
 
@@ -704,7 +733,13 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipEventElapsedTime(&ms, ev[3], ev[19]));
     p.sweep_ms = ms;
     for (int s = 0; s < 16; ++s) {
-        HIPCHK(hipEventElapsedTime(&ms, ev[3 + s], ev[(s == 15) ? 19 : 4 + s]));
+        if (!evrec(s)) {
+            p.sweep_launch_ms[s] = 0.f;   // inside sweep 0's launch
+            continue;
+        }
+        int e = s + 1;   // the next recorded event
+        while (e < 16 && !evrec(e)) ++e;
+        HIPCHK(hipEventElapsedTime(&ms, ev[3 + s], ev[(e >= 16) ? 19 : 3 + e]));
         p.sweep_launch_ms[s] = ms;
     }
     HIPCHK(hipEventElapsedTime(&ms, ev[19], ev[20]));
@@ -1016,10 +1051,10 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     const u64 init_key = ((u64)__builtin_bit_cast(uint32_t, init) << 32) | 0xffffffffull;
     hipEvent_t *ev = S->ev;
     HIPCHK(hipEventRecord(ev[0], st));
-    HIPCHK(hipMemsetAsync(S->err_flag, 0, sizeof(int), st));
-    HIPCHK(hipMemsetAsync(S->evals, 0, sizeof(unsigned long long), st));
-    if (S->wf.ctrl) HIPCHK(hipMemsetAsync(S->wf.ctrl + 1, 0, 3 * sizeof(int), st));
-    if (S->sp.ctl) HIPCHK(hipMemsetAsync(S->sp.ctl, 0, SP_NCTL * sizeof(u64), st));
+    HIPCHK(zero_async(S->err_flag, sizeof(int), st));
+    HIPCHK(zero_async(S->evals, sizeof(unsigned long long), st));
+    if (S->wf.ctrl) HIPCHK(zero_async(S->wf.ctrl + 1, 3 * sizeof(int), st));
+    if (S->sp.ctl) HIPCHK(zero_async(S->sp.ctl, SP_NCTL * sizeof(u64), st));
     if (ntri) {
         hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, d_tri, ntri, d_xyz, nvert,
                            S->soup, S->err_flag);
@@ -1404,6 +1439,7 @@ int sdfgen_hip_release(void)
         hipFree(w->xyz);
         hipFree(w->err_flag);
         hipFree(w->evals);
+        hipFree(w->status);
         hipFree(w->out);
         tile_sweep_release(w->wf);
         sparse_sweep_release(w->sp);

@@ -929,7 +929,7 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
         if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
     }
     // per sweep: reset the list counters; error bits and statistics accumulate over the call
-    if (hipMemsetAsync(W.ctl + SP_QUEUE, 0, (SP_DIAGX - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
+    if (zero_async(W.ctl + SP_QUEUE, (SP_DIAGX - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
         return -4;
     blocks = (n + 255) / 256;
     if (blocks > 16384) blocks = 16384;

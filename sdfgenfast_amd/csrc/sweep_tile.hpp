@@ -1081,7 +1081,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     int ti = -1;
     if (int rc = st_prepare(W, st, ni, nj, cs, ce, &ti)) return fail(rc, "buffer or task table allocation failed");
     if (++W.epoch == 0) ++W.epoch;   // 0 = never published
-    if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+    if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     StParams P;
     P.soup = soup;
     P.cell = cell;
@@ -1372,7 +1372,7 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     }
     if (prepare_only) return 0;   // buffers and tables in place (Z-slabs: before anything is enqueued)
     if (++W.mepoch == 0) ++W.mepoch;   // completion flags of this launch (0 = never)
-    if (hipMemsetAsync(W.ctrl, 0, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+    if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     StParams P;
     memset(&P, 0, sizeof(P));
     P.soup = soup;

@@ -1,6 +1,7 @@
 """Second-pass diagnostics: per-sweep launch times and repair counters of one workload
 (run with SDFGEN_LIB_OVERRIDE=ab/spprof.so for the SP_PROF cycle split)."""
 import sys, os
+os.environ.setdefault("SDFGEN_SWEEP_EVENTS", "1")   # per-sweep launch times (the library's default times them together)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sdfgenfast_amd import _lib, meshgen
 
