@@ -134,6 +134,9 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 constexpr int BAND_BT = BAND_BT_DEF;    // triangles per batch (<= 64: one wave sets a batch up)
 constexpr int BAND_LDS = BAND_LDS_DEF;  // u64 keys in the LDS table (40 KB)
 static_assert(BAND_BT >= 1 && BAND_BT <= 64, "a batch's boxes are scanned by one wave");
+// pair_of's binary search halves from BAND_BT / 2: it reaches every triangle only for a power of two
+// (BAND_BT_DEF=48 measured a digest mismatch at C3: triangle 47 of a batch was never paired)
+static_assert((BAND_BT & (BAND_BT - 1)) == 0, "BAND_BT must be a power of two");
 
 struct BandBox {
     int i0, j0, k0, bi, bj, bk;         // clamped band box (bi*bj*bk cells; 0 = empty)
