@@ -82,7 +82,9 @@ def cpu_baseline(workload: str):
         return {"value": round(n / el / 1e6, 4), "unit": "Mvoxels/s", "cores": th, "kind": "reference",
                 "sample": f"reference cpu_lib make_level_set3 (oracle/_ref, built from /root/reference), "
                           f"num_threads={th}, the full {workload} workload ({n} voxels, {t.shape[0]} triangles), "
-                          f"{el:.2f} s; 1 thread: tests/golden/hashes.json ref_seconds_1thread"}
+                          f"{el:.2f} s; 1 thread: tests/golden/hashes.json ref_seconds_1thread. Timing only: with "
+                          f"{th} threads the reference's k-split sweep races (SURVEY K1), so its output is not "
+                          f"parity-valid (the parity target is its 1-thread result)"}
     log("bench: oracle/_ref (the reference build) is absent -- timing the native CPU backend instead")
     t0 = time.perf_counter()
     _lib.cpu_make_level_set3(v, t, o, dx, *dims, 1, th, _lib.LAYOUT_ARRAY3)
@@ -254,6 +256,11 @@ def step_latency(dev):
     return best
 
 
+def _build_id():
+    from sdfgenfast_amd import _lib
+    return _lib.build_id()
+
+
 def roofline(r, step_us, workload):
     achieved = r["bytes_per_launch"] / (r["launch_ms"] * 1e-3) / 1e9 if r["launch_ms"] > 0 else 0.0
     traffic, traffic_src = None, None
@@ -261,8 +268,11 @@ def roofline(r, step_us, workload):
     if os.path.exists(tp):
         rec = json.load(open(tp))
         k = rec.get("kernels", {}).get("k_sweep_tile")
-        if rec.get("workload") == workload and k and r["dims"] == tuple(rec.get("dims", r["dims"])):
-            traffic, traffic_src = k["hbm_bytes_per_launch"], "profiles/pmc_summary.json"
+        if rec.get("workload") == workload and k:
+            if rec.get("build_id") == _build_id():
+                traffic, traffic_src = k["hbm_bytes_per_launch"], f"profiles/pmc_summary.json (build {rec['build_id']})"
+            else:   # counters of another build of the library: not this run's traffic
+                traffic_src = f"stale: profiles/pmc_summary.json is of build {rec.get('build_id')}, not {_build_id()}"
     lat = None
     if step_us and r["chain_steps"] > 0 and r["launch_ms"] > 0:
         bound_ms = r["chain_steps"] * step_us * 1e-3
@@ -289,10 +299,13 @@ def valu(r, workload):
     k = next((v for n, v in rec.get("kernels", {}).items() if n.startswith("k_sweep_tile")), None)
     if rec.get("workload") != workload or not k or "SQ_INSTS_VALU" not in k:
         return None
+    if rec.get("build_id") != _build_id():
+        return {"kernel": "k_sweep_tile", "insts_per_launch": None, "frac": None,
+                "source": f"stale: profiles/pmc_sq_summary.json is of build {rec.get('build_id')}, not {_build_id()}"}
     rate = k["SQ_INSTS_VALU"] / (r["launch_ms"] * 1e-3)
     return {"kernel": "k_sweep_tile", "insts_per_launch": int(k["SQ_INSTS_VALU"]), "achieved": round(rate / 1e9, 2),
             "peak": round(VALU_ISSUE_PEAK / 1e9, 1), "unit": "G wave-instructions/s",
-            "frac": round(rate / VALU_ISSUE_PEAK, 4), "source": "profiles/pmc_sq_summary.json"}
+            "frac": round(rate / VALU_ISSUE_PEAK, 4), "source": f"profiles/pmc_sq_summary.json (build {rec['build_id']})"}
 
 
 def summary(r, world, mode, t1_ms=None):
@@ -427,8 +440,14 @@ def main():
             "phases_ms": r["phases"],
             "sweep_impl": r["sweep_impl"],
             "parity": r["parity"],
+            "build_id": _build_id(),
         }
         res.update(res_side)
+        if "host" in res_side:
+            # SURVEY 8.d's definition of t: one call with host arrays in and a host Array3f out
+            # (PCIe included), next to the HBM-resident `value`
+            res["value_host_io"] = res_side["host"]["value"]
+            res["ms_per_call_host_io"] = res_side["host"]["ms_per_call"]
         if zs_err:
             res["zslab_error"] = zs_err
         if world == 1 and not args.no_cpu_baseline:

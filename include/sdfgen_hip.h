@@ -60,6 +60,11 @@ enum {
 
 int sdfgen_hip_abi_version(void);
 
+/* Build identity: the first 16 hex digits of the SHA-256 of the sources and build files this
+ * library was compiled from (sdfgenfast_amd/Makefile).  No reference counterpart; bench.py uses it
+ * to match PMC counter summaries to the library that produced the timed numbers. */
+const char *sdfgen_hip_build_id(void);
+
 /* Number of visible HIP devices (0 when none; never an error).
  * Replaces sdfgen::is_gpu_available() (common/sdfgen_unified.cpp:19-28). */
 int sdfgen_hip_device_count(void);

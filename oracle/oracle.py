@@ -23,10 +23,12 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _ORACLE_SO = os.path.join(_HERE, "liboracle.so")
 _REF_SO = os.path.join(_HERE, "_ref", "libsdfref.so")
+_MESHREF_SO = os.path.join(_HERE, "_ref", "libmeshref.so")
 
 _P = ctypes.c_void_p
 _oracle = None
 _ref = None
+_meshref = None
 
 
 def build(ref: bool = False) -> None:
@@ -167,3 +169,48 @@ def ref_ptd_batch(pts: np.ndarray) -> np.ndarray:
     out = np.empty(pts.shape[0], np.float32)
     ref_lib().ref_ptd_batch(pts.shape[0], _ptr(pts), _ptr(out))
     return out
+
+
+def meshref_available() -> bool:
+    return os.path.exists(_MESHREF_SO)
+
+
+def meshref_lib():
+    global _meshref
+    if _meshref is None:
+        if not os.path.exists(_MESHREF_SO):
+            raise FileNotFoundError(f"{_MESHREF_SO} not built (needs /root/reference; `make -C oracle ref`)")
+        L = ctypes.CDLL(_MESHREF_SO)
+        L.ref_mesh_load.argtypes = [ctypes.c_char_p, ctypes.POINTER(_P)]
+        L.ref_mesh_load.restype = ctypes.c_int
+        L.ref_mesh_info.argtypes = [_P, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), _P]
+        L.ref_mesh_info.restype = None
+        L.ref_mesh_copy.argtypes = [_P, _P, _P]
+        L.ref_mesh_copy.restype = None
+        L.ref_mesh_log.argtypes = [_P]
+        L.ref_mesh_log.restype = ctypes.c_char_p
+        L.ref_mesh_free.argtypes = [_P]
+        L.ref_mesh_free.restype = None
+        _meshref = L
+    return _meshref
+
+
+def ref_load_mesh(path: str):
+    """The REFERENCE loader meshio::load_mesh (common/mesh_io.cpp:29-48) ->
+    (rc, vertices (N,3) f32, triangles (M,3) u32, bounds (6,) f32 = min_box, max_box, log);
+    rc 1 = loaded, 0 = the reference returned false, 2 = it threw (a bad OBJ face index).
+    The vectors are whatever the reference left in them, also when it failed."""
+    L = meshref_lib()
+    h = _P()
+    ok = L.ref_mesh_load(os.fsencode(path), ctypes.byref(h))
+    try:
+        nv, nt = ctypes.c_uint64(), ctypes.c_uint64()
+        b = np.empty(6, np.float32)
+        L.ref_mesh_info(h, ctypes.byref(nv), ctypes.byref(nt), _ptr(b))
+        v = np.empty((nv.value, 3), np.float32)
+        t = np.empty((nt.value, 3), np.uint32)
+        L.ref_mesh_copy(h, _ptr(v), _ptr(t))
+        log = L.ref_mesh_log(h).decode(errors="replace")
+    finally:
+        L.ref_mesh_free(h)
+    return int(ok), v, t, b, log

@@ -26,6 +26,7 @@ _u64 = ctypes.c_uint64
 # Every symbol include/sdfgen_hip.h declares (checked by tests/test_abi.py).
 EXPORTED = (
     "sdfgen_hip_abi_version",
+    "sdfgen_hip_build_id",
     "sdfgen_hip_device_count",
     "sdfgen_hip_make_level_set3",
     "sdfgen_hip_make_level_set3_device",
@@ -97,6 +98,7 @@ def _load():
             "(python -c 'import __graft_entry__ as g; g.build()' or make -C sdfgenfast_amd)")
     L = ctypes.CDLL(LIB_PATH)
     L.sdfgen_hip_abi_version.restype = ctypes.c_int
+    L.sdfgen_hip_build_id.restype = ctypes.c_char_p
     L.sdfgen_hip_device_count.restype = ctypes.c_int
     L.sdfgen_hip_make_level_set3.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
@@ -195,6 +197,11 @@ def mesh_load(path: str, fmt: int = MESH_AUTO):
     finally:
         lib.sdfgen_mesh_free(h)
     return v, t, b, f.value
+
+
+def build_id() -> str:
+    """The loaded library's build identity (sdfgen_hip_build_id: SHA-256 prefix of its sources)."""
+    return lib.sdfgen_hip_build_id().decode()
 
 
 def device_count() -> int:

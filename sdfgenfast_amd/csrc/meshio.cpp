@@ -7,12 +7,18 @@
 // line boundaries, with the reference's line grammar and its results bit for bit:
 //   * numbers: `istream >> float` is a correctly rounded decimal conversion of the longest
 //     numeric prefix (libstdc++ num_get + strtof in the C locale); std::from_chars is the same
-//     conversion, locale-free.  num_get accepts a leading '+', no "inf"/"nan" and no hex.
+//     conversion, locale-free.  num_get accepts a leading '+', no "inf"/"nan" (with or without
+//     a sign) and no hex, and FAILS on an exponent marker with no digits ("1e", "2E+"): it
+//     consumes the 'e' and the sign, and strtof then does not use the whole token.
 //   * OBJ faces: v, v/vt, v/vt/vn, v//vn -- the index before the first '/' through std::stoi
 //     semantics (leading whitespace, optional sign, digits; an invalid token is an error), then
 //     1-based -> 0-based as uint32 (wrapping), fan triangulation (mesh_io_obj.cpp:115-121).
-//   * bounds: update_minmax per accepted vertex in file order (common/util.h:299-303: a value
-//     that lowers the minimum does not also raise the maximum), computed in one ordered pass.
+//   * bounds: meshio::update_minmax per accepted vertex (common/mesh_io.h:101-108: std::min and
+//     std::max applied independently; the non-template overload wins over util.h's else-if one),
+//     computed in one ordered pass.
+//   * a binary STL with 0 facets loads as an empty mesh (mesh_io_stl.cpp:140-172 returns true).
+// All of this is pinned against the reference loaders compiled from their sources
+// (tests/test_meshio_ref.py, oracle/mesh_ref_shim.cpp).
 #include "sdfgen_meshio.h"
 
 #include <algorithm>
@@ -72,7 +78,8 @@ inline bool parse_float(const char *&p, const char *end, float &v)
     if (p >= end) return false;
     const char *q = p;
     if (*q == '+') ++q;   // num_get takes a leading '+', from_chars does not
-    if (q < end && (*q == 'i' || *q == 'I' || *q == 'n' || *q == 'N')) return false;   // no inf / nan
+    const char *m = q < end && (*q == '+' || *q == '-') ? q + 1 : q;
+    if (m < end && (*m == 'i' || *m == 'I' || *m == 'n' || *m == 'N')) return false;   // no [+-]inf / nan
     if (q + 1 < end && q[0] == '0' && (q[1] == 'x' || q[1] == 'X')) {   // num_get reads "0", stops at 'x'
         v = 0.0f;
         if (*p == '-') v = -0.0f;
@@ -93,6 +100,14 @@ inline bool parse_float(const char *&p, const char *end, float &v)
         const float w = strtof(tok, nullptr);
         if (w == std::numeric_limits<float>::infinity() || w == -std::numeric_limits<float>::infinity()) return false;
         v = w;
+    }
+    if (r.ptr < end && (*r.ptr == 'e' || *r.ptr == 'E')) {
+        // from_chars stopped at an exponent marker: either the token already had its exponent
+        // ("1e2e3": num_get stops there too) or the marker has no digits, which num_get consumes
+        // and then fails on.
+        bool had_exp = false;
+        for (const char *c = s; c < r.ptr; ++c) had_exp |= *c == 'e' || *c == 'E';
+        if (!had_exp) return false;
     }
     p = r.ptr;
     return true;
@@ -189,6 +204,8 @@ void parse_obj_chunk(const char *b, const char *e, ObjPart &out)
     }
 }
 
+// meshio::update_minmax (common/mesh_io.h:101-108) over the vertices in file order:
+// min = std::min(min, x) = (x < min) ? x : min, max = std::max(max, x) = (max < x) ? x : max.
 void update_bounds(const std::vector<float> &xyz, float b[6])
 {
     for (int c = 0; c < 3; ++c) {
@@ -200,7 +217,7 @@ void update_bounds(const std::vector<float> &xyz, float b[6])
         for (int c = 0; c < 3; ++c) {
             const float x = xyz[3 * v + c];
             if (x < b[c]) b[c] = x;
-            else if (x > b[3 + c]) b[3 + c] = x;
+            if (b[3 + c] < x) b[3 + c] = x;
         }
 }
 
@@ -246,8 +263,7 @@ int load_binary_stl(const std::vector<char> &buf, sdfgen_mesh &m, char *errbuf, 
         m.tri[3 * t + 1] = (uint32_t)(3 * t + 1);
         m.tri[3 * t + 2] = (uint32_t)(3 * t + 2);
     }
-    if (n == 0) return fail(errbuf, errlen, SDFGEN_MESH_EFORMAT, "No faces found in STL file");
-    return 0;
+    return 0;   // n == 0: an empty mesh, as the reference returns (no "no faces" check for binary)
 }
 
 inline bool starts_ci(const char *p, const char *e, const char *kw)

@@ -56,6 +56,22 @@ struct Err {
     }
 };
 
+// Every C-ABI entry point that selects a device restores the caller's current device on return
+// (success or error): the reference runs on, and leaves, the current device
+// (gpu_lib/makelevelset3_gpu.cu:600-603), so a later call on the current device must not land on
+// whichever GPU an earlier multi-device call touched last.
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard()
+    {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
 #define HIPCHK(expr)                                                                            \
     do {                                                                                        \
         hipError_t e_ = (expr);                                                                 \
@@ -1354,6 +1370,7 @@ int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
                                const float origin[3], float dx, int ni, int nj, int nk, int exact_band, int ngpu,
                                int out_layout, float *phi_out, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (errbuf && errlen) errbuf[0] = 0;
     int rc = validate(ntri, nvert, dx, ni, nj, nk, out_layout, err);
@@ -1404,6 +1421,7 @@ int sdfgen_hip_make_level_set3_device(int device, const uint32_t *d_tri, uint64_
                                       int exact_band, int out_layout, float *d_phi_out, void *hip_stream,
                                       char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (errbuf && errlen) errbuf[0] = 0;
     int rc = validate(ntri, nvert, dx, ni, nj, nk, out_layout, err);
@@ -1432,6 +1450,7 @@ int sdfgen_hip_last_profile(sdfgen_hip_profile *out)
 
 int sdfgen_hip_release(void)
 {
+    DeviceGuard dg_;
     std::lock_guard<std::mutex> lk(g_mu);
     for (Workspace *w : g_ws) {
         hipSetDevice(w->device);
@@ -1456,6 +1475,7 @@ int sdfgen_hip_release(void)
 
 int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries, uint64_t *n_out)
 {
+    DeviceGuard dg_;
     Err err{nullptr, 0};
     *n_out = 0;
     Workspace *ws = nullptr;
@@ -1476,6 +1496,7 @@ int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries
 int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, float *out, char *errbuf,
                          size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "no GPU device %d", device);
     HIPCHK(hipSetDevice(device));
@@ -1493,6 +1514,7 @@ int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, 
 
 int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *out4, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "no GPU device %d", device);
     HIPCHK(hipSetDevice(device));
@@ -1514,6 +1536,7 @@ int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *ou
 int sdfgen_hip_slab_create(int device, int nslabs, int slab, int ni, int nj, int nk, sdfgen_hip_slab **out,
                            char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (errbuf && errlen) errbuf[0] = 0;
     if (!out) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
@@ -1552,6 +1575,7 @@ int sdfgen_hip_slab_range(const sdfgen_hip_slab *h, int *k_begin, int *k_end)
 
 int sdfgen_hip_slab_export(sdfgen_hip_slab *h, void *handle, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (!h || !handle) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
     static_assert(sizeof(hipIpcMemHandle_t) <= SDFGEN_HIP_IPC_HANDLE_BYTES, "IPC handle size");
@@ -1566,6 +1590,7 @@ int sdfgen_hip_slab_export(sdfgen_hip_slab *h, void *handle, char *errbuf, size_
 int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *h, const void *lower, const void *upper, char *errbuf,
                                 size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
     SlabSession *S = &h->s;
@@ -1595,6 +1620,7 @@ int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *h, const void *lower, const voi
 int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *h, sdfgen_hip_slab *lower, sdfgen_hip_slab *upper, char *errbuf,
                                   size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
     SlabSession *S = &h->s;
@@ -1619,6 +1645,7 @@ int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *h, const uint32_t *d_tri, uint64_t 
                             uint64_t nvert, const float origin[3], float dx, int exact_band, int out_layout,
                             float *d_phi_slab, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (errbuf && errlen) errbuf[0] = 0;
     if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
@@ -1634,6 +1661,7 @@ int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *h, const uint32_t *d_tri, uint64_t 
 
 int sdfgen_hip_slab_prepare(sdfgen_hip_slab *h, uint64_t ntri, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (errbuf && errlen) errbuf[0] = 0;
     if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
@@ -1643,6 +1671,7 @@ int sdfgen_hip_slab_prepare(sdfgen_hip_slab *h, uint64_t ntri, char *errbuf, siz
 
 int sdfgen_hip_slab_finish(sdfgen_hip_slab *h, uint64_t nvert, sdfgen_hip_profile *prof, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
     std::lock_guard<std::mutex> lk(h->s.mu);
@@ -1654,6 +1683,7 @@ int sdfgen_hip_slab_run(sdfgen_hip_slab *h, const uint32_t *tri, uint64_t ntri, 
                         const float origin[3], float dx, int exact_band, int out_layout, float *phi_slab,
                         sdfgen_hip_profile *prof, char *errbuf, size_t errlen)
 {
+    DeviceGuard dg_;
     Err err{errbuf, errlen};
     if (errbuf && errlen) errbuf[0] = 0;
     if (!h) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
@@ -1686,6 +1716,7 @@ int sdfgen_hip_slab_run(sdfgen_hip_slab *h, const uint32_t *tri, uint64_t ntri, 
 
 int sdfgen_hip_slab_debug_dump(sdfgen_hip_slab *h, int which, void *out, uint64_t max_bytes, uint64_t *n_bytes)
 {
+    DeviceGuard dg_;
     if (!h || !out || !n_bytes) return SDFGEN_HIP_EINVAL;
     SlabSession *S = &h->s;
     if (hipSetDevice(S->device) != hipSuccess || hipStreamSynchronize(S->stream) != hipSuccess) return SDFGEN_HIP_ERUNTIME;
@@ -1704,6 +1735,7 @@ int sdfgen_hip_slab_debug_dump(sdfgen_hip_slab *h, int which, void *out, uint64_
 
 int sdfgen_hip_slab_destroy(sdfgen_hip_slab *h)
 {
+    DeviceGuard dg_;
     if (!h) return 0;
     slab_free(&h->s);
     delete h;

@@ -1,18 +1,13 @@
 """Host-side mesh and .sdf file I/O (the callers either side of the hot path).
 
 * ``load_mesh``  -- the library's native loaders (include/sdfgen_meshio.h,
-  csrc/meshio.cpp: whole-file read, OBJ parsed in parallel line chunks, correctly
-  rounded from_chars floats, update_minmax bounds in file order).  ``load_mesh_py``
-  is the line-by-line Python restatement kept as the tests' second opinion.
-
-These restate the reference's loaders/writers with bulk I/O instead of
-per-value stream calls:
-
-* ``load_mesh_py``  -- common/mesh_io.cpp:29-48 dispatch on extension;
-  binary STL common/mesh_io_stl.cpp:98-173 (no vertex de-duplication:
-  vertices 3t, 3t+1, 3t+2 per facet), ASCII STL :179-303, format detection
-  :42-92, OBJ common/mesh_io_obj.cpp:21-157 (fan triangulation :115-121).
-  Bounds follow update_minmax (common/mesh_io.h:101-108).
+  csrc/meshio.cpp: whole-file read, text parsed in parallel line chunks, correctly
+  rounded from_chars floats, update_minmax bounds in file order), restating
+  common/mesh_io.cpp:29-48 (dispatch on extension), binary STL
+  common/mesh_io_stl.cpp:98-173 (no vertex de-duplication), ASCII STL :179-303,
+  format detection :42-92, OBJ common/mesh_io_obj.cpp:21-157 (fan :115-121), bounds
+  common/mesh_io.h:101-108.  Pinned bit for bit to the reference loaders compiled
+  from their sources (tests/test_meshio_ref.py).
 * ``write_sdf`` / ``read_sdf`` -- common/sdf_io.cpp:10-147: a 36-byte header
   (3 x int32 dims, 3 x f32 min, 3 x f32 max = min + n*dx) followed by float32
   data written k-fastest (for i, for j, for k), i.e. exactly a C-ordered
@@ -21,152 +16,10 @@ per-value stream calls:
 """
 from __future__ import annotations
 
-import ctypes
 import os
 import struct
 
 import numpy as np
-
-_STL_HEADER = 80
-_STL_TRI = 50
-_FLT_MAX = np.finfo(np.float32).max
-
-_libc = ctypes.CDLL(None)
-_libc.strtof.restype = ctypes.c_float
-_libc.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
-
-
-def _parse_f32(tok: str) -> np.float32:
-    """`istream >> float` on one token: strtof's correct rounding (float(tok) then a cast to
-    float32 would double-round); ValueError where the stream would fail -- nothing numeric,
-    inf / nan (num_get does not read them) or an overflow; "0x..." reads as 0 (num_get stops
-    at the 'x')."""
-    t = tok.lstrip("+") if tok.startswith("+") and not tok.startswith("+-") else tok
-    low = t.lstrip("-").lower()
-    if low.startswith(("inf", "nan")):
-        raise ValueError(f"not a number: {tok!r}")
-    if low.startswith("0x"):
-        return np.float32(-0.0) if t.startswith("-") else np.float32(0.0)
-    b = t.encode()
-    buf = ctypes.create_string_buffer(b)
-    end = ctypes.c_char_p()
-    v = _libc.strtof(buf, ctypes.byref(end))
-    used = ctypes.cast(end, ctypes.c_void_p).value - ctypes.addressof(buf)
-    if used <= 0 or not np.isfinite(v):
-        raise ValueError(f"not a number: {tok!r}")
-    return np.float32(v)
-
-
-def _bounds(v: np.ndarray):
-    """update_minmax over the vertices in order (common/util.h:299-303): a value that lowers
-    the minimum does not also raise the maximum, NaN never updates either."""
-    mn = np.full(3, _FLT_MAX, np.float32)
-    mx = np.full(3, -_FLT_MAX, np.float32)
-    for c in range(3):
-        x = v[:, c].astype(np.float32)
-        if x.size == 0:
-            continue
-        # prefix minimum BEFORE each vertex; vertex k lowers the minimum iff x_k < that
-        pre = np.minimum.accumulate(np.concatenate([[_FLT_MAX], np.where(np.isnan(x), _FLT_MAX, x)]))[:-1]
-        lowers = x < pre
-        mn[c] = np.float32(np.nanmin(np.concatenate([[_FLT_MAX], x])))
-        cand = x[~lowers & ~np.isnan(x)]
-        if cand.size:
-            mx[c] = max(np.float32(-_FLT_MAX), np.float32(cand.max()))
-    return (tuple(float(a) for a in mn), tuple(float(a) for a in mx))
-
-
-def _stl_is_binary(path: str) -> bool:
-    with open(path, "rb") as f:
-        head = f.read(_STL_HEADER)
-        if len(head) < 5:
-            raise RuntimeError(f"Failed to load mesh: {path}")
-        if not head.lower().startswith(b"solid"):
-            return True
-        cnt = f.read(4)
-        if len(cnt) < 4:
-            return False
-        (n,) = struct.unpack("<I", cnt)
-    return os.path.getsize(path) == _STL_HEADER + 4 + n * _STL_TRI
-
-
-def _load_binary_stl(path: str):
-    with open(path, "rb") as f:
-        f.seek(_STL_HEADER)
-        cnt = f.read(4)
-        if len(cnt) < 4:
-            raise RuntimeError(f"Failed to load mesh: {path}")
-        (n,) = struct.unpack("<I", cnt)
-        raw = np.fromfile(f, dtype=np.uint8, count=n * _STL_TRI)
-    if raw.size < n * _STL_TRI:
-        raise RuntimeError(f"Failed to load mesh: {path} (truncated binary STL)")
-    rec = raw.reshape(n, _STL_TRI)
-    verts = rec[:, 12:48].copy().view("<f4").reshape(n * 3, 3).astype(np.float32)
-    tris = np.arange(n * 3, dtype=np.uint32).reshape(n, 3)
-    return verts, tris
-
-
-def _load_ascii_stl(path: str):
-    verts = []
-    ntri = 0
-    in_facet = in_loop = False
-    nv = 0
-    with open(path, "r", errors="replace") as f:
-        for line in f:
-            s = line.strip()
-            low = s.lower()
-            if low.startswith("facet"):
-                in_facet, nv = True, 0
-            elif low.startswith("endfacet"):
-                if nv != 3:
-                    raise RuntimeError(f"Failed to load mesh: {path} (facet with {nv} vertices)")
-                in_facet = False
-                ntri += 1
-            elif low.startswith("outer loop"):
-                in_loop = True
-            elif low.startswith("endloop"):
-                in_loop = False
-            elif low.startswith("vertex"):
-                if not (in_facet and in_loop):
-                    raise RuntimeError(f"Failed to load mesh: {path} (vertex outside facet)")
-                tok = s.split()
-                if len(tok) < 4:
-                    raise RuntimeError(f"Failed to load mesh: {path} (bad vertex line)")
-                verts.append([_parse_f32(t) for t in tok[1:4]])
-                nv += 1
-    if not verts or ntri == 0:
-        raise RuntimeError(f"Failed to load mesh: {path} (no facets)")
-    v = np.asarray(verts, dtype=np.float32).reshape(-1, 3)
-    t = np.arange(ntri * 3, dtype=np.uint32).reshape(ntri, 3)
-    return v, t
-
-
-def _load_obj(path: str):
-    verts = []
-    faces = []
-    with open(path, "r", errors="replace") as f:
-        for line in f:
-            line = line.rstrip("\n").rstrip("\r")
-            if not line:
-                continue
-            if line[0] == "v" and len(line) > 1 and line[1] in " \t":
-                tok = line.split()
-                if len(tok) < 4:
-                    continue
-                try:
-                    verts.append([_parse_f32(t) for t in tok[1:4]])
-                except ValueError:
-                    continue   # mesh_io_obj.cpp:77-80: warn and skip the line
-            elif line[0] == "f" and len(line) > 1 and line[1] in " \t":
-                idx = [int(t.split("/")[0]) for t in line.split()[1:]]
-                if len(idx) < 3:
-                    continue
-                for q in range(1, len(idx) - 1):  # fan, mesh_io_obj.cpp:115-121
-                    faces.append([(idx[0] - 1) & 0xFFFFFFFF, (idx[q] - 1) & 0xFFFFFFFF,
-                                  (idx[q + 1] - 1) & 0xFFFFFFFF])
-    if not verts or not faces:
-        raise RuntimeError(f"Failed to load mesh: {path} (no vertices or faces)")
-    return np.asarray(verts, np.float32).reshape(-1, 3), np.asarray(faces, np.uint32).reshape(-1, 3)
 
 
 def load_mesh(filename: str):
@@ -184,24 +37,6 @@ def load_mesh(filename: str):
     except RuntimeError as e:
         raise RuntimeError(f"Failed to load mesh: {path} ({e})") from e
     return v, t, (tuple(float(a) for a in b[:3]), tuple(float(a) for a in b[3:]))
-
-
-def load_mesh_py(filename: str):
-    """Python restatement of the reference loaders (slow; the tests' cross-check of load_mesh)."""
-    path = os.fspath(filename)
-    ext = os.path.splitext(path)[1].lower()
-    if not os.path.isfile(path):
-        raise RuntimeError(f"Failed to load mesh: {path}")
-    try:
-        if ext == ".stl":
-            v, t = _load_binary_stl(path) if _stl_is_binary(path) else _load_ascii_stl(path)
-        elif ext == ".obj":
-            v, t = _load_obj(path)
-        else:
-            raise RuntimeError(f"Failed to load mesh: {path} (unsupported format {ext})")
-    except (ValueError, UnicodeDecodeError) as e:
-        raise RuntimeError(f"Failed to load mesh: {path} ({e})") from e
-    return v, t, _bounds(v)
 
 
 def write_sdf(filename: str, sdf: np.ndarray, origin, dx: float) -> int:

@@ -28,20 +28,29 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 from oracle import oracle as O  # noqa: E402
-from sdfgenfast_amd import meshgen, meshio  # noqa: E402
+from sdfgenfast_amd import meshgen  # noqa: E402
 
 RES = "/root/reference/tests/resources"
+
+
+def _ref_load(path):
+    """The reference's own loader (common/mesh_io.cpp via oracle/_ref/libmeshref.so). The native
+    loader gives the same bits on these files (tests/test_meshio_ref.py::test_reference_resources_live),
+    so fixtures made before round 3 with meshio.load_mesh are unchanged."""
+    rc, v, t, _, _ = O.ref_load_mesh(path)
+    assert rc == 1, path
+    return v, t, None
 
 
 def small_cases():
     """(name, vertices, triangles, origin, dx, (ni,nj,nk), exact_band)."""
     cases = []
-    v, t, _ = meshio.load_mesh(os.path.join(RES, "test_x3y4z5_bin.stl"))
+    v, t, _ = _ref_load(os.path.join(RES, "test_x3y4z5_bin.stl"))
     o, dx = meshgen.grid_mode2b(v, 32, 32, 32, 1)
     cases.append(("x3y4z5_stl_32", v, t, o, dx, (32, 32, 32), 1))           # SURVEY 8.c fixture (1)
     o, dx, dims = meshgen.grid_proportional(v, 32, 1)
     cases.append(("x3y4z5_stl_prop32", v, t, o, dx, dims, 1))               # 32x42x52
-    vq, tq, _ = meshio.load_mesh(os.path.join(RES, "test_x3y4z5_quads.obj"))
+    vq, tq, _ = _ref_load(os.path.join(RES, "test_x3y4z5_quads.obj"))
     o, dx = meshgen.grid_mode2b(vq, 24, 20, 28, 2)
     cases.append(("x3y4z5_quads_obj", vq, tq, o, dx, (24, 20, 28), 1))
     vc, tc = meshgen.unit_cube()

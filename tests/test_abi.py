@@ -17,7 +17,7 @@ def declared_functions():
     for h in ("sdfgen_hip.h", "sdfgen_cpu.h", "sdfgen_meshio.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-        names |= set(re.findall(r"^\s*(?:int|void)\s+(sdfgen_\w+)\s*\(", src, flags=re.M))
+        names |= set(re.findall(r"^\s*(?:int|void|const char \*)\s*(sdfgen_\w+)\s*\(", src, flags=re.M))
     return sorted(names)
 
 
@@ -38,6 +38,15 @@ def test_cxx_dropin_symbols_exported():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
     assert "_ZN6sdfgen15make_level_set3" in out
     assert "_ZN6sdfgen16is_gpu_availableEv" in out
+
+
+def test_build_id_matches_sources():
+    """The library's embedded identity is the Makefile's hash of the current sources: a stale
+    library (sources edited, not rebuilt) is detectable, and PMC summaries are matched on it."""
+    want = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "sdfgenfast_amd"), "build-id"],
+                          capture_output=True, text=True, check=True).stdout.strip()
+    assert re.fullmatch(r"[0-9a-f]{16}", want)
+    assert _lib.build_id() == want
 
 
 def test_abi_version_and_device_count():

@@ -120,6 +120,17 @@ def test_slabs_middle_slabs_in_process(nslabs, dims):
     assert r.returncode == 0 and r.stdout.startswith("OK"), r.stdout + r.stderr[-3000:]
 
 
+@pytest.mark.parametrize("name", ["c4_sphere1m_512", "c5_sphere4m_1024"])
+def test_two_slabs_full_size_match_reference_digest(name):
+    """north_star's Z-slab configurations at full size (C4 512^3; C5 1024^3 = 1.07G cells, past
+    2^31: the slab offsets cell_mem - plane * k_begin and the 64-bit indices), two slabs on this
+    box's one GPU in one process, against the reference's SHA-256 of phi."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8", SDFGEN_TILE_GRID="192")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"),
+                        "2", name, "1"], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 # One process per slab, inboxes mapped with HIP IPC.  Two processes only: more processes
 # sharing one GPU's hardware queues are not guaranteed to run their kernels concurrently.
 @pytest.mark.parametrize("nslabs,dims", [(2, (40, 36, 44)), (2, (19, 23, 31))])

@@ -1,6 +1,7 @@
 """Load rate of the native OBJ / ASCII-STL / binary-STL loaders on the C3 mesh (1,000,000-triangle
-bumpy sphere written as files), against the Python restatement (meshio.load_mesh_py) on the same
-files.  python tools/meshio_rate.py [outdir]"""
+bumpy sphere written as files), against the REFERENCE loaders compiled from their sources
+(oracle/_ref/libmeshref.so: common/mesh_io*.cpp; development container only) on the same files.
+python tools/meshio_rate.py [outdir]"""
 import os
 import sys
 import tempfile
@@ -9,6 +10,7 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 
+from oracle import oracle as O  # noqa: E402
 from sdfgenfast_amd import meshgen, meshio  # noqa: E402
 
 
@@ -33,11 +35,12 @@ def main():
         vn, tn, bn = meshio.load_mesh(path)
         tnat = time.perf_counter() - t0
         t0 = time.perf_counter()
-        vp, tp, bp = meshio.load_mesh_py(path)
-        tpy = time.perf_counter() - t0
-        same = np.array_equal(vn.view(np.uint32), vp.view(np.uint32)) and np.array_equal(tn, tp) and bn == bp
+        rc, vr, tr, br, _ = O.ref_load_mesh(path)
+        tref = time.perf_counter() - t0
+        same = (rc == 1 and np.array_equal(vn.view(np.uint32), vr.view(np.uint32)) and np.array_equal(tn, tr)
+                and np.array_equal(np.float32(bn[0] + bn[1]).view(np.uint32), br.view(np.uint32)))
         print(f"{os.path.basename(path)}: {os.path.getsize(path) / 1e6:.0f} MB, {tn.shape[0]} triangles: native "
-              f"{tnat:.3f} s, python {tpy:.2f} s, identical={same}", flush=True)
+              f"{tnat:.3f} s, reference {tref:.2f} s, identical={same}", flush=True)
 
 
 if __name__ == "__main__":

@@ -9,7 +9,14 @@ for f in glob.glob("gpurun_out/pmc_sq/**/*counter_collection.csv", recursive=Tru
         n = r["Kernel_Name"].split("(")[0].split("::")[-1][:40]
         per[n][r["Counter_Name"]] += float(r["Counter_Value"]); disp[n].add(r["Dispatch_Id"])
 import json, os
-out = {"workload": sys.argv[1], "units": "per launch (summed over the chip's counter instances)", "kernels": {}}
+bid = None
+for line in reversed(open("gpurun_out/pmc_sq.log").read().splitlines()):
+    if line.startswith("{"):
+        bid = json.loads(line).get("build_id")
+        break
+if not bid:
+    sys.exit("gpurun_out/pmc_sq.log has no bench line with a build_id")
+out = {"workload": sys.argv[1], "build_id": bid, "units": "per launch (summed over the chip's counter instances)", "kernels": {}}
 for n, c in per.items():
     d = len(disp[n])
     print(f"{n:42s} launches {d:3d} " + " ".join(f"{k}={v/d:.4g}" for k, v in sorted(c.items())))

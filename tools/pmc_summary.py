@@ -31,14 +31,25 @@ def load(counter):
     return out
 
 
+def build_id_of(log):
+    """The library build id the pass ran with: bench.py's JSON line in the pass's log."""
+    for line in reversed(open(log).read().splitlines()):
+        if line.startswith("{"):
+            return json.loads(line).get("build_id")
+    return None
+
+
 fetch, write = load("FETCH_SIZE"), load("WRITE_SIZE")
+ids = {build_id_of(os.path.join(ROOT, "gpurun_out", f"pmc_{c}.log")) for c in ("FETCH_SIZE", "WRITE_SIZE")}
+if len(ids) != 1 or None in ids:
+    sys.exit(f"pmc passes ran with different or unknown library builds: {ids}")
 kern = {}
 for k in sorted(set(fetch) | set(write)):
     f = sum(fetch.get(k, [0])) / max(len(fetch.get(k, [])), 1) * 1024.0
     w = sum(write.get(k, [0])) / max(len(write.get(k, [])), 1) * 1024.0
     kern[k] = {"launches_fetch": len(fetch.get(k, [])), "launches_write": len(write.get(k, [])),
                "fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": int(2 * f + w)}
-res = {"workload": work, "units": "bytes per launch; FETCH_SIZE doubled (gfx950 wide-read correction)",
+res = {"workload": work, "build_id": ids.pop(), "units": "bytes per launch; FETCH_SIZE doubled (gfx950 wide-read correction)",
        "note": "8-byte and byte-sized accesses are uncalibrated widths; Infinity-Cache hits are counted",
        "kernels": kern}
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
