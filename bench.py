@@ -173,6 +173,22 @@ def measure_single(workload, steps, warmup, dev, verify=True, dist=None):
     return r
 
 
+def _slab_phases(p):
+    """Where one slab's time went in its last timed call (device wall-clock phase timers,
+    include/sdfgen_hip.h slab_*): the first pass's tile launch, the boundary tiles' waits on the
+    upstream GPU, and per second-pass sweep the DONE / READY handshakes, the repair kernel and its
+    inbound-ring draining."""
+    r3 = lambda xs: [round(x, 4) for x in xs]
+    it, ot = p["slab_inbox_tasks"], p["slab_other_tasks"]
+    return {"first_pass_ms": round(p["sweep_launch_ms"][0], 4),
+            "second_pass_ms": round(sum(p["sweep_launch_ms"][8:]), 4),
+            "inbox_tasks": it, "inbox_idle_ms_per_task": round(p["slab_inbox_idle_ms"] / it, 4) if it else None,
+            "other_tasks": ot, "other_idle_ms_per_task": round(p["slab_other_idle_ms"] / ot, 4) if ot else None,
+            "wait_done_ms": r3(p["slab_wait_done_ms"]), "wait_ready_ms": r3(p["slab_wait_ready_ms"]),
+            "repair_ms": r3(p["slab_repair_ms"]), "inbound_ms": r3(p["slab_inbound_ms"]),
+            "inbound_entries": list(p["slab_inbound_entries"])}
+
+
 def measure_zslab(workload, steps, warmup, dev, dist, world, rank, verify=True):
     """One grid split into `world` Z-slabs, one per rank/GPU (sdfgenfast_amd.distributed)."""
     from sdfgenfast_amd import _hiprt, _lib, meshgen
@@ -198,6 +214,9 @@ def measure_zslab(workload, steps, warmup, dev, dist, world, rank, verify=True):
          "sweeps_per_launch": spl, "launches": launches, "sweep_impl": profs[-1]["sweep_impl"],
          "chain_steps": profs[-1]["chain_steps"],
          "bytes_per_launch": SWEEP_BYTES_PER_CELL * A * B * (sess.k_end - sess.k_begin) * spl, "parity": None}
+    phases = [None] * world
+    dist.all_gather_object(phases, dict(_slab_phases(profs[-1]), rank=rank, k_range=[sess.k_begin, sess.k_end]))
+    r["slab_phases"] = phases
     if verify:
         rec = _golden(workload)
         got = out.download(np.float32, out.nbytes // 4)
@@ -315,6 +334,8 @@ def summary(r, world, mode, t1_ms=None):
     if t1_ms:
         d["single_gpu_ms"] = round(t1_ms, 3)
         d["efficiency"] = round(t1_ms / (world * r["ms_per_step"]), 4)
+    if r.get("slab_phases"):
+        d["slab_phases"] = r["slab_phases"]
     return d
 
 
@@ -442,6 +463,8 @@ def main():
             "parity": r["parity"],
             "build_id": _build_id(),
         }
+        if r.get("slab_phases"):
+            res["slab_phases"] = r["slab_phases"]   # per rank: where each slab's time went
         res.update(res_side)
         if "host" in res_side:
             # SURVEY 8.d's definition of t: one call with host arrays in and a host Array3f out

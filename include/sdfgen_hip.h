@@ -36,7 +36,7 @@ extern "C" {
 /* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
 #pragma GCC visibility push(default)
 
-#define SDFGEN_HIP_ABI_VERSION 2   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare */
+#define SDFGEN_HIP_ABI_VERSION 3   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers */
 
 enum {
     SDFGEN_HIP_OK = 0,
@@ -129,6 +129,17 @@ typedef struct sdfgen_hip_profile {
     int slabs;                /* Z-slabs the grid was split into (0 or 1: one device) */
     double chain_steps;       /* modelled critical path of the first-pass launch, in tile steps (the
                                  latency roofline's chain length; 0 without the overlapped launch) */
+    /* Z-slab phase timers of the last call on this slab (device wall clock; all 0 on one device).
+     * Second-pass sweep 9 + m, m = 0..7: */
+    double slab_wait_done_ms[8];     /* waiting for the neighbours' DONE of the previous sweep (longer side) */
+    double slab_wait_ready_ms[8];    /* waiting for their READY (live halos initialised) */
+    double slab_repair_ms[8];        /* the repair kernel: first workgroup's start .. last wave's exit */
+    double slab_inbound_ms[8];       /* its inbound lanes: until the upstream slab's repair ended, entries taken */
+    uint64_t slab_inbound_entries[8];   /* inbound-ring entries taken (upstream boundary cells that relabelled) */
+    /* First pass: */
+    double slab_inbox_idle_ms;       /* helper-wave idle time of the tasks reading the upstream GPU's inbox, summed */
+    double slab_other_idle_ms;       /* the same for the other tasks */
+    uint64_t slab_inbox_tasks, slab_other_tasks;
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

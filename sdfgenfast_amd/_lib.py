@@ -83,11 +83,22 @@ class Profile(ctypes.Structure):
         ("tile_multi", ctypes.c_int),
         ("slabs", ctypes.c_int),
         ("chain_steps", ctypes.c_double),
+        ("slab_wait_done_ms", ctypes.c_double * 8),
+        ("slab_wait_ready_ms", ctypes.c_double * 8),
+        ("slab_repair_ms", ctypes.c_double * 8),
+        ("slab_inbound_ms", ctypes.c_double * 8),
+        ("slab_inbound_entries", ctypes.c_uint64 * 8),
+        ("slab_inbox_idle_ms", ctypes.c_double),
+        ("slab_other_idle_ms", ctypes.c_double),
+        ("slab_inbox_tasks", ctypes.c_uint64),
+        ("slab_other_tasks", ctypes.c_uint64),
     ]
 
     def as_dict(self):
         d = {f: getattr(self, f) for f, _ in self._fields_}
-        d["sweep_launch_ms"] = list(self.sweep_launch_ms)
+        for f, t in self._fields_:
+            if hasattr(t, "_length_"):
+                d[f] = list(getattr(self, f))
         return d
 
 

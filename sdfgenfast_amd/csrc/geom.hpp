@@ -81,6 +81,22 @@ __device__ __forceinline__ unsigned long long sdf_chk(unsigned site, unsigned lo
 #define SDF_CHK(site, x, lo, hi) (x)
 #endif
 
+// Z-slab phase timers (SlabSession::tm, zeroed per call; wall_clock64 ticks unless a count): where
+// a slab's time goes around its neighbours, reported per rank by the N > 1 bench line.
+enum : int {
+    TM_WAIT_DONE = 0,      // [8] k_sp_slab_wait(DONE) spin per second-pass sweep (the longer side)
+    TM_WAIT_READY = 8,     // [8] k_sp_slab_wait(READY) spin
+    TM_REPAIR = 16,        // [8] k_sp_recheck: workgroup 0's start .. the last wave's exit
+    TM_INBOUND = 24,       // [8] inbound lanes: start .. the upstream slab's DONE seen and its COUNT drained
+    TM_INBOUND_N = 32,     // [8] inbound-ring entries taken (count)
+    TM_REPAIR_T0 = 40,     // [8] scratch: workgroup 0's start stamp
+    TM_INBOX_IDLE = 48,    // first pass: helper-wave idle ticks of the tasks reading the upstream inbox
+    TM_INBOX_TASKS = 49,   //   ... their number
+    TM_OTHER_IDLE = 50,    // first pass: helper-wave idle ticks of the other tasks
+    TM_OTHER_TASKS = 51,   //   ... their number
+    TM_N = 64
+};
+
 SDF_HD uint32_t lo_word(int label, int lc) { return ((uint32_t)lc << LBL_BITS) | ((uint32_t)label & LBL_MASK); }
 SDF_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 

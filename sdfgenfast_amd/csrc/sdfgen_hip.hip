@@ -861,6 +861,7 @@ struct SlabSession {
     int *err_flag = nullptr;
     unsigned *arrive = nullptr;
     unsigned long long *evals = nullptr;
+    unsigned long long *tm = nullptr;     // phase timers (geom.hpp TM_*), zeroed per call
     size_t cap_soup = 0, cap_tri = 0, cap_xyz = 0, cap_out = 0;
     TileSweepWorkspace wf;
     SparseSweepWorkspace sp;
@@ -911,6 +912,7 @@ int slab_alloc(SlabSession *S, Err &err)
     HIPCHK(hipMalloc((void **)&S->err_flag, sizeof(int)));
     HIPCHK(hipMalloc((void **)&S->evals, sizeof(unsigned long long)));
     HIPCHK(hipMalloc((void **)&S->arrive, sizeof(unsigned)));
+    HIPCHK(hipMalloc((void **)&S->tm, TM_N * sizeof(unsigned long long)));
     // The communication block is written by the NEIGHBOUR GPUs (system-scope stores over xGMI,
     // through an IPC or peer mapping) while this GPU's kernels poll it.  Plain hipMalloc memory
     // is coarse-grained: HIP makes remote writes to it visible only at kernel boundaries (an L2
@@ -941,6 +943,7 @@ void slab_free(SlabSession *S)
     (void)hipFree(S->err_flag);
     (void)hipFree(S->evals);
     (void)hipFree(S->arrive);
+    (void)hipFree(S->tm);
     (void)hipFree(S->comm);
     tile_sweep_release(S->wf);
     sparse_sweep_release(S->sp);
@@ -1072,6 +1075,8 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     HIPCHK(hipEventRecord(ev[0], st));
     HIPCHK(zero_async(S->err_flag, sizeof(int), st));
     HIPCHK(zero_async(S->evals, sizeof(unsigned long long), st));
+    HIPCHK(zero_async(S->tm, TM_N * sizeof(unsigned long long), st));
+    S->wf.tm = S->tm;
     if (S->wf.ctrl) HIPCHK(zero_async(S->wf.ctrl + 1, 3 * sizeof(int), st));
     if (S->sp.ctl) HIPCHK(zero_async(S->sp.ctl, SP_NCTL * sizeof(u64), st));
     if (ntri) {
@@ -1180,6 +1185,8 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
             L.prev_epoch = S->sync_epoch;
             L.epoch = ++S->sync_epoch;
             L.arrive = S->arrive;
+            L.tm = S->tm;
+            L.tm_m = m;
             if (int rc = sparse_sweep_slab(S->sp, st, S->soup, L, origin, dx, ni, nj, nk, s))
                 return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse sweep setup failed");
             S->launches += 3;
@@ -1217,8 +1224,9 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
 {
     hipStream_t st = S->stream;
     int flag = 0, wf_err[2] = {0, 0};
-    unsigned long long evals = 0, sp_ctl[4] = {0, 0, 0, 0};
+    unsigned long long evals = 0, sp_ctl[4] = {0, 0, 0, 0}, tm[TM_N];
     HIPCHK(hipMemcpyAsync(&flag, S->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(tm, S->tm, sizeof(tm), hipMemcpyDeviceToHost, st));
     if (S->wf.ctrl) HIPCHK(hipMemcpyAsync(wf_err, S->wf.ctrl + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
     if (S->sparse_sweeps && S->sp.ctl) HIPCHK(hipMemcpyAsync(sp_ctl, S->sp.ctl, sizeof(sp_ctl), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&evals, S->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
@@ -1257,6 +1265,21 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         p.tile_multi = S->tile_multi;
         p.chain_steps = S->tile_multi ? S->wf.chain_steps : 0.0;
         p.slabs = S->nslabs;
+        int khz = 0;   // device wall clock (wall_clock64) rate
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, S->device) != hipSuccess || khz <= 0)
+            khz = 100000;
+        const double tick_ms = 1.0 / khz;
+        for (int m = 0; m < 8; ++m) {
+            p.slab_wait_done_ms[m] = tm[TM_WAIT_DONE + m] * tick_ms;
+            p.slab_wait_ready_ms[m] = tm[TM_WAIT_READY + m] * tick_ms;
+            p.slab_repair_ms[m] = tm[TM_REPAIR + m] * tick_ms;
+            p.slab_inbound_ms[m] = tm[TM_INBOUND + m] * tick_ms;
+            p.slab_inbound_entries[m] = tm[TM_INBOUND_N + m];
+        }
+        p.slab_inbox_idle_ms = tm[TM_INBOX_IDLE] * tick_ms;
+        p.slab_other_idle_ms = tm[TM_OTHER_IDLE] * tick_ms;
+        p.slab_inbox_tasks = tm[TM_INBOX_TASKS];
+        p.slab_other_tasks = tm[TM_OTHER_TASKS];
         *prof = p;
     }
     if (wf_err[0] & 4)

@@ -136,6 +136,8 @@ struct SpParams {
     unsigned long long *up_flags, *down_flags;   // the neighbours' flag words (remote; null: none)
     unsigned long long epoch;          // this sweep's synchronisation epoch
     unsigned long long ntri;           // triangles in the soup (bounds-checked builds)
+    unsigned long long *tm;            // Z-slab phase timers (TM_*; null: not recorded)
+    int tm_m;                          // second-pass sweep index 0..7 for tm
 };
 
 __device__ __forceinline__ unsigned long long sp_ld64(const unsigned long long *p)
@@ -423,14 +425,20 @@ __device__ __forceinline__ void sp_append_issue(const SpParams &P, unsigned shar
         asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_nop 1" : "=&v"(A.old_q) : "v"(w), "v"(d) : "memory");
     }
 }
+// The wait is unconditional (a scalar instruction every path from the loop top passes, live or
+// not), so that the ISA check tools/check_split_append.py (run by tests/test_split_append_asm.py on
+// every build) can prove statically that no instruction names the atomic's destination registers
+// before it: the compiler's wait-count pass does not see the asm atomic.  Not live, it costs nothing
+// extra -- by then every iteration's vector memory operations have been waited for by the returning
+// atomics around it.
 __device__ __forceinline__ void sp_append_finish(const SpParams &P, unsigned shard, const size_t (&tgt)[7], SpAppend &A)
 {
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(A.old_q)::"memory");   // the returned word has landed
     if (!A.live) return;
     A.live = false;
     const unsigned lane = threadIdx.x & 63;
     unsigned long long t0 = 0;
     if (lane == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(A.old_q)::"memory");   // the returned word has landed
         t0 = A.old_q & 0xffffffffull;
         if (t0 + A.tot > SP_TAIL_LIMIT) atomicOr(&P.ctl[SP_ERR], 2ull);
     }
@@ -620,9 +628,15 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
     unsigned long long *const q_tail = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];   // pending << 32 | tail
     unsigned long long *const q_head = q_tail + 16;
     unsigned *const ring = P.queue + (size_t)shard * P.cap;
+    unsigned long long t_start = 0, n_in = 0;   // Z-slab phase timers (TM_*)
+    if (SLAB && P.tm) {
+        t_start = wall_clock64();
+        if (blockIdx.x == 0 && lane == 0) P.tm[TM_REPAIR_T0 + P.tm_m] = t_start;
+    }
 #if SP_SPLIT_APPEND
     SpAppend app;
     app.live = false;
+    app.old_q = 0;   // read by the unconditional wait of sp_append_finish before the first issue
     size_t tgt_app[7];   // the cells of the append in flight
 #endif
     for (;;) {
@@ -663,6 +677,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 __hip_atomic_store(P.in_ring + h_in, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 in_wait = false;
                 in_spins = 0;
+                ++n_in;
                 const unsigned u = v - 1;   // an upstream cell: its downstream cells here are queued
                 const int iu = (int)(u % (unsigned)P.ni);
                 const unsigned ru = u / (unsigned)P.ni;
@@ -674,6 +689,10 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 in_role = false;   // DONE is written after COUNT: nothing more can come
                 sp_order();
                 atomicAdd(&P.ctl[SP_INDONE], 1ull);
+                if (P.tm) {
+                    atomicMax(P.tm + TM_INBOUND + P.tm_m, wall_clock64() - t_start);
+                    if (n_in) atomicAdd(P.tm + TM_INBOUND_N + P.tm_m, n_in);
+                }
             } else if (++in_spins > SP_WATCHDOG || ((in_spins & 255u) == 255u && (sp_ld64(&P.ctl[SP_ERR]) & 16ull))) {
                 atomicOr(&P.ctl[SP_ERR], 16ull);
                 in_role = false;
@@ -756,6 +775,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
     if (SLAB) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every push of this wave has landed
         if ((threadIdx.x & 63) == 0 && atomicAdd(&P.ctl[SP_EXIT], 1ull) == gridDim.x - 1ull) {
+            if (P.tm) P.tm[TM_REPAIR + P.tm_m] = wall_clock64() - sp_ld64(P.tm + TM_REPAIR_T0 + P.tm_m);
             if (P.down_flags) {
                 __hip_atomic_store(P.down_flags + (SP_FL_COUNT + P.up_side) * SP_FL_STRIDE, sp_ld64(&P.ctl[SP_OUTTAIL]),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -790,12 +810,15 @@ struct SpHaloParams {
     int word;                                  // k_sp_slab_wait: SP_FL_DONE or SP_FL_READY
     unsigned long long *ctl;                   // sparse control words (error bits)
     unsigned *arrive;                          // zeroed before k_sp_slab_halo
+    unsigned long long *tm;                    // Z-slab phase timers (TM_*; null: not recorded)
+    int tm_m;                                  // second-pass sweep index 0..7
 };
 
 __global__ void __launch_bounds__(64) k_sp_slab_wait(SpHaloParams H)
 {
     if (threadIdx.x >= 2 || !H.nb_flags[threadIdx.x]) return;
     const unsigned long long *f = H.flags + (H.word + threadIdx.x) * SP_FL_STRIDE;
+    const unsigned long long t0 = wall_clock64();
     for (unsigned spins = 0;; ++spins) {
         if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= H.epoch) break;
         // fail fast once a handshake of this call has already failed (the neighbour is not coming)
@@ -806,6 +829,7 @@ __global__ void __launch_bounds__(64) k_sp_slab_wait(SpHaloParams H)
         if (spins < 64) __builtin_amdgcn_s_sleep(2);
         else __builtin_amdgcn_s_sleep(16);
     }
+    if (H.tm) atomicMax(H.tm + (H.word == SP_FL_DONE ? TM_WAIT_DONE : TM_WAIT_READY) + H.tm_m, wall_clock64() - t0);
 }
 
 __global__ void __launch_bounds__(256) k_sp_slab_halo(SpHaloParams H)
@@ -1026,6 +1050,8 @@ struct SpSlabSweep {
     unsigned long long *nb_flags[2];   // the neighbours' (null: no neighbour)
     unsigned long long prev_epoch, epoch;
     unsigned *arrive;                  // one local word (the halo kernel's arrival counter)
+    unsigned long long *tm;            // phase timers (TM_*; null: none) and this sweep's index 0..7
+    int tm_m;
 };
 
 inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, const SpSlabSweep &L,
@@ -1048,6 +1074,8 @@ inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const floa
     H.flags = L.flags;
     H.ctl = W.ctl;
     H.arrive = L.arrive;
+    H.tm = L.tm;
+    H.tm_m = L.tm_m;
     H.word = SP_FL_DONE;
     H.epoch = L.prev_epoch;
     hipLaunchKernelGGL(k_sp_slab_wait, dim3(1), dim3(64), 0, st, H);
@@ -1074,6 +1102,8 @@ inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const floa
     P.up_flags = L.nb_flags[up];
     P.down_flags = L.nb_flags[down];
     P.epoch = L.epoch;
+    P.tm = L.tm;
+    P.tm_m = L.tm_m;
     const char *stg = getenv("SDFGEN_DEBUG_SPARSE_STAGE");   // diagnostics: stop after kernel n (1 halo .. 4 all)
     const int stage = stg ? atoi(stg) : 4;
     if (stage >= 2) hipLaunchKernelGGL(k_sp_jacobi<true>, dim3((unsigned)blocks), dim3(256), 0, st, P);

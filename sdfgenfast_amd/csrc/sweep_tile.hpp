@@ -93,7 +93,10 @@ constexpr int ST_G = ST_G_DEF;
 static_assert(ST_NCW >= 1 && ST_NCW <= 3 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
 static_assert(!ST_TWIN || ST_CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
 typedef int i4v __attribute__((ext_vector_type(4)));
-static_assert((ST_RR & (ST_RR - 1)) == 0 && ST_RR >= 8, "ring slots: power of two >= 8 (RR = 4 measured wrong results: no lead left between the waves)");
+// Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
+// neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the lead
+// between them (RR = 4 with 2 waves measured wrong results: no lead left).
+static_assert((ST_RR & (ST_RR - 1)) == 0 && (ST_RR >= 8 || (ST_NCW == 1 && ST_RR == 4)), "ring slots: power of two, >= 8 (>= 4 with one compute wave)");
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
 constexpr int ST_LEAD = ST_RR - 4;            // max lead of wave w over wave w+1 (ring hazard)
@@ -162,6 +165,7 @@ struct StParams {
     unsigned *done;               // [task] = call_epoch once the task's cell stores are visible
     unsigned call_epoch;
     StSweep sw[ST_MAXSW];
+    unsigned long long *tm;       // Z-slab phase timers (sweep_sparse.hpp TM_*; null: not recorded)
 };
 
 __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
@@ -784,6 +788,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
             static_assert(ST_G == 4 || ST_G == 2, "helper pipeline is written out for 2- or 4-element batches");
             unsigned idle = 0;
+            unsigned long long t_idle = 0;   // Z-slab: wall ticks this helper spent backing off (TM_*)
             for (;;) {
                 // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
                 // may finish step h while wave w-1 is still on step h (it needs only h-1 of it).
@@ -809,9 +814,11 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                             if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
                             break;
                         }
+                        const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
                         if (idle < 4) __builtin_amdgcn_s_sleep(1);
                         else if (idle < 16) __builtin_amdgcn_s_sleep(4);
                         else __builtin_amdgcn_s_sleep(ST_HSLEEP);
+                        if (SLAB && P.tm) t_idle += wall_clock64() - ts;
                         continue;
                     }
                 }
@@ -935,10 +942,16 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
                         break;
                     }
+                    const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
                     if (idle < 4) __builtin_amdgcn_s_sleep(1);
                     else if (idle < 16) __builtin_amdgcn_s_sleep(4);
                     else __builtin_amdgcn_s_sleep(ST_HSLEEP);
+                    if (SLAB && P.tm) t_idle += wall_clock64() - ts;
                 }
+            }
+            if (SLAB && P.tm && L == 0) {   // where the slab boundary's tiles wait for the upstream GPU
+                atomicAdd(P.tm + (inbox ? TM_INBOX_IDLE : TM_OTHER_IDLE), t_idle);
+                atomicAdd(P.tm + (inbox ? TM_INBOX_TASKS : TM_OTHER_TASKS), 1ull);
             }
         }
         if (MULTI) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every wave's cell stores done
@@ -969,6 +982,7 @@ struct TileSweepWorkspace {
     int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
     bool skip_seen = true;     // the "already examined" skip (diagnostics can turn it off)
     unsigned long long clo = 0, chi = ~0ull, ntri = ~0ull;   // address bounds for bounds-checked builds
+    unsigned long long *tm = nullptr;   // Z-slab phase timers (owned by the slab session; null: none)
     size_t cap_hb = 0, cap_hc = 0;
     // task tables (dequeue order) for up to two tile grids: a Z-slab alternates between
     // two c extents (k-up and k-down sweeps), and a table must not be rewritten while a
@@ -1405,6 +1419,7 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     P.deps = W.mdeps;
     P.done = W.mdone;
     P.call_epoch = W.mepoch;
+    P.tm = nsl > 1 ? W.tm : nullptr;
     for (int q = 0; q < ns; ++q) {
         const int sw = s0 + q, *d = dirs[sw % 8];
         const size_t x = (size_t)q * nsl + me;

@@ -10,4 +10,5 @@ $H --offload-arch=gfx950 $F -c sdfgenfast_amd/csrc/sdfgen_hip.hip -o ab/build_$1
 $H -x hip --offload-arch=gfx950 $(echo $F | sed "s#-mllvm [^ ]*##g") -c sdfgenfast_amd/csrc/cpu_backend.cpp -o ab/build_$1/b.o
 $H $(echo $F | sed "s#-mllvm [^ ]*##g") -c sdfgenfast_amd/csrc/sdfgen_unified.cpp -o ab/build_$1/c.o
 $H $(echo $F | sed "s#-mllvm [^ ]*##g") -c sdfgenfast_amd/csrc/meshio.cpp -o ab/build_$1/d.o
+$H -O2 -std=c++17 -fPIC -Iinclude -DSDFGEN_BUILD_ID="\"ab-$1\"" -c sdfgenfast_amd/csrc/build_id.cpp -o ab/build_$1/e.o
 $H --offload-arch=gfx950 -shared -fPIC -o ab/$1.so ab/build_$1/*.o -lpthread
