@@ -156,7 +156,7 @@ def measure_single(workload, steps, warmup, dev, verify=True, dist=None):
     r = {"workload": workload, "dims": dims, "triangles": int(t.shape[0]), "ms_per_step": el / steps * 1e3,
          "value": ni * nj * nk * steps / el / 1e6, "phases": ph, "launch_ms": launch_ms,
          "sweeps_per_launch": spl, "launches": launches, "sweep_impl": profs[-1]["sweep_impl"],
-         "chain_steps": profs[-1]["chain_steps"],
+         "chain_steps": profs[-1]["chain_steps"], "tile_cfg": profs[-1]["tile_cfg"],
          "bytes_per_launch": SWEEP_BYTES_PER_CELL * A * B * C * spl, "parity": None}
     if verify:
         rec = _golden(workload)
@@ -331,6 +331,8 @@ def summary(r, world, mode, t1_ms=None):
     d = {"workload": r["workload"], "n_gpus": world, "parallelism": mode, "value": round(r["value"], 3),
          "unit": "Mvoxels/s", "ms_per_step": round(r["ms_per_step"], 3), "phases_ms": r["phases"],
          "parity": r["parity"]}
+    if "tile_cfg" in r:
+        d["tile_cfg"] = r["tile_cfg"]
     if t1_ms:
         d["single_gpu_ms"] = round(t1_ms, 3)
         d["efficiency"] = round(t1_ms / (world * r["ms_per_step"]), 4)
@@ -460,6 +462,7 @@ def main():
             "valu": valu(r, args.workload) if world == 1 else None,
             "phases_ms": r["phases"],
             "sweep_impl": r["sweep_impl"],
+            "tile_cfg": r.get("tile_cfg"),
             "parity": r["parity"],
             "build_id": _build_id(),
         }

@@ -36,7 +36,7 @@ extern "C" {
 /* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
 #pragma GCC visibility push(default)
 
-#define SDFGEN_HIP_ABI_VERSION 3   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers */
+#define SDFGEN_HIP_ABI_VERSION 3   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers, tile_cfg */
 
 enum {
     SDFGEN_HIP_OK = 0,
@@ -140,6 +140,8 @@ typedef struct sdfgen_hip_profile {
     double slab_inbox_idle_ms;       /* helper-wave idle time of the tasks reading the upstream GPU's inbox, summed */
     double slab_other_idle_ms;       /* the same for the other tasks */
     uint64_t slab_inbox_tasks, slab_other_tasks;
+    int tile_cfg;                    /* first-pass tile kernel: 0 = 2 compute waves x 32 cells (latency-bound
+                                        grids), 1 = 1 compute wave x 64 cells (throughput-bound grids) */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

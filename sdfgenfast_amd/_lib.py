@@ -92,6 +92,7 @@ class Profile(ctypes.Structure):
         ("slab_other_idle_ms", ctypes.c_double),
         ("slab_inbox_tasks", ctypes.c_uint64),
         ("slab_other_tasks", ctypes.c_uint64),
+        ("tile_cfg", ctypes.c_int),
     ]
 
     def as_dict(self):

@@ -782,6 +782,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sparse_sweeps = sparse_sweeps;
     p.tile_multi = multi_n;
     p.chain_steps = multi_n > 1 ? ws->wf.chain_steps : 0.0;
+    p.tile_cfg = multi_n > 1 && ws->wf.thr ? 1 : 0;
     p.slabs = 1;
     p.sparse_first = sparse_sweeps ? sparse_first : 16;
 #ifdef SP_JACOBI_COUNT
@@ -886,8 +887,10 @@ int slab_preload_kernels(Err &err)
 {
     if (getenv("SDFGEN_NO_KERNEL_PRELOAD")) return 0;   // diagnostics
     const void *k[] = {(const void *)k_prep_soup, (const void *)k_init, (const void *)k_band_lds,
-                       (const void *)k_sign, (const void *)k_sweep_tile<true, false, false>,
-                       (const void *)k_sweep_tile<true, false, true>, (const void *)k_sp_jacobi<true>,
+                       (const void *)k_sign, (const void *)k_sweep_tile<StCfgLat, true, false, false>,
+                       (const void *)k_sweep_tile<StCfgLat, true, false, true>,
+                       (const void *)k_sweep_tile<StCfgThr, true, false, false>,
+                       (const void *)k_sweep_tile<StCfgThr, true, false, true>, (const void *)k_sp_jacobi<true>,
                        (const void *)k_sp_jlist<true>, (const void *)k_sp_recheck<true>, (const void *)k_sp_slab_wait,
                        (const void *)k_sp_slab_halo, (const void *)k_sp_slab_export};
     for (const void *f : k) {
@@ -1264,6 +1267,7 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         p.sparse_claims = sp_ctl[SP_ENQ];
         p.tile_multi = S->tile_multi;
         p.chain_steps = S->tile_multi ? S->wf.chain_steps : 0.0;
+        p.tile_cfg = S->tile_multi && S->wf.thr ? 1 : 0;
         p.slabs = S->nslabs;
         int khz = 0;   // device wall clock (wall_clock64) rate
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, S->device) != hipSuccess || khz <= 0)

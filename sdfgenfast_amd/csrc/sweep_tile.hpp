@@ -83,28 +83,54 @@ namespace sdfhip {
 constexpr int ST_T = 8;                       // tile edge (b and c)
 constexpr int ST_NCOL = ST_T * ST_T;          // 64 columns
 constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edge (8), corner
-constexpr int ST_NCW = ST_NCW_DEF;
-constexpr int ST_CLW = ST_T / ST_NCW;         // c-columns per compute wave
-constexpr int ST_CPW = ST_T * ST_CLW;         // cells per compute wave
-constexpr int ST_RR = ST_RR_DEF;
 constexpr int ST_RO = ST_RO_DEF;
 constexpr int ST_RH = ST_RH_DEF;
 constexpr int ST_G = ST_G_DEF;
-static_assert(ST_NCW >= 1 && ST_NCW <= 3 && ST_T % ST_NCW == 0, "compute waves must split the tile's c-columns");
-static_assert(!ST_TWIN || ST_CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
 typedef int i4v __attribute__((ext_vector_type(4)));
-// Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
-// neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the lead
-// between them (RR = 4 with 2 waves measured wrong results: no lead left).
-static_assert((ST_RR & (ST_RR - 1)) == 0 && (ST_RR >= 8 || (ST_NCW == 1 && ST_RR == 4)), "ring slots: power of two, >= 8 (>= 4 with one compute wave)");
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
-constexpr int ST_LEAD = ST_RR - 4;            // max lead of wave w over wave w+1 (ring hazard)
-constexpr int ST_THREADS = 64 * (ST_NCW + 1); // compute waves + helper wave
-constexpr int ST_RING0 = 0;                                   // RR slots x 64 columns
-constexpr int ST_HALO0 = ST_RING0 + ST_RR * ST_NCOL;          // 17 streams x RH
-constexpr int ST_OWN0 = ST_HALO0 + ST_NSTREAM * ST_RH;        // RO slots x 64 columns
-constexpr int ST_ENTS = ST_OWN0 + ST_RO * ST_NCOL;
+
+// Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, and the
+// waves per SIMD the register budget must allow.
+template <int NCW_, int RR_, bool TWIN_, int WPE_>
+struct StCfg {
+    static constexpr int NCW = NCW_;                    // compute waves per tile
+    static constexpr int CLW = ST_T / NCW;              // c-columns per compute wave
+    static constexpr int CPW = ST_T * CLW;              // cells per compute wave
+    static constexpr int RR = RR_;                      // neighbour ring slots
+    static constexpr bool TWIN = TWIN_;                 // lane L + 32 is the twin of cell lane L
+    static constexpr int WPE = WPE_;
+    static constexpr int LEAD = NCW > 1 ? RR - 4 : 0;   // max lead of wave w over wave w+1 (ring hazard)
+    static constexpr int THREADS = 64 * (NCW + 1);      // compute waves + helper wave
+    static constexpr int RING0 = 0;                                 // RR slots x 64 columns
+    static constexpr int HALO0 = RING0 + RR * ST_NCOL;              // 17 streams x RH
+    static constexpr int OWN0 = HALO0 + ST_NSTREAM * ST_RH;         // RO slots x 64 columns
+    static constexpr int ENTS = OWN0 + ST_RO * ST_NCOL;
+    static_assert(NCW >= 1 && NCW <= 3 && ST_T % NCW == 0, "compute waves must split the tile's c-columns");
+    static_assert(!TWIN || CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
+    // Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
+    // neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the
+    // lead between them (RR = 4 with 2 waves measured wrong results: no lead left).
+    static_assert((RR & (RR - 1)) == 0 && (RR >= 8 || (NCW == 1 && RR == 4)), "ring slots: power of two, >= 8 (4 with one compute wave)");
+};
+// Latency-bound grids (few tiles per sweep for the chip, C3): 2 compute waves of 32 cells with twin
+// lanes -- the shortest step; ~47 KB LDS, 3 tiles per CU.  Throughput-bound grids (C4, C5): ONE
+// compute wave of 64 cells, no ring lead -- half the instructions per cell; ~35 KB LDS, 4 tiles per
+// CU (first pass 512^3: 50.2 -> 44.5 ms, 1024^3: 342 -> 272 ms; 256^3: 13.75 -> 14.6 ms).
+using StCfgLat = StCfg<ST_NCW_DEF, ST_RR_DEF, (ST_TWIN != 0), ST_WPE_DEF>;
+#ifndef ST_THR_WPE
+#define ST_THR_WPE 2
+#endif
+using StCfgThr = StCfg<1, 4, false, ST_THR_WPE>;
+
+// The configuration of a launch with `tiles` tasks per sweep: the throughput one once a sweep offers
+// well over the chip's resident 2-wave tiles (3 per CU).  SDFGEN_TILE_CFG=0/1 forces one (tests, A/B).
+inline bool st_use_thr(long long tiles)
+{
+    if (const char *e = getenv("SDFGEN_TILE_CFG")) return atoi(e) == 1;
+    return tiles > 2048;
+}
+
 constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
 
 // Entry layout in LDS: [3e] = (x1, w), [3e+1] = (x2, phi -- own entries only), [3e+2] = x3,
@@ -146,7 +172,7 @@ struct StParams {
     int di, dj, dk;
     unsigned epoch;
     int sweep;
-    int lead;                     // max steps wave w may run ahead of wave w+1 (<= ST_LEAD)
+    int lead;                     // max steps wave w may run ahead of wave w+1 (<= Cfg::LEAD)
     // Z-slab mode (one GPU per slab of the grid).  Tiles cover oriented c in
     // [cs, ce); the plane c = cs-1 of an upstream slab arrives in hc_in, and this slab's plane
     // c = ce-1 is published to the downstream slab's inbox hc_out.  An inbox holds one granule
@@ -248,9 +274,12 @@ __device__ __forceinline__ void st_load_tri(const float4 *soup, int t, float4 &v
 // MULTI: one launch runs the tasks of several consecutive sweeps (the first pass), each task
 // first waiting for the tiles of the previous sweep whose cells it reads or overwrites; the
 // task order is topological, so every awaited tile is already claimed.
-template <bool SLAB, bool TRACE, bool MULTI = false>
-__global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams P0)
+template <class Cfg, bool SLAB, bool TRACE, bool MULTI = false>
+__global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams P0)
 {
+    constexpr int ST_NCW = Cfg::NCW, ST_CLW = Cfg::CLW, ST_CPW = Cfg::CPW, ST_RR = Cfg::RR, ST_THREADS = Cfg::THREADS,
+                  ST_RING0 = Cfg::RING0, ST_HALO0 = Cfg::HALO0, ST_OWN0 = Cfg::OWN0, ST_ENTS = Cfg::ENTS;
+    constexpr bool TWIN = Cfg::TWIN;
     StParams P = P0;
     constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
@@ -406,7 +435,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
             // ======================= compute waves =======================
             // Wave w owns the ST_CLW c-columns from ST_CLW * w on: lanes 0..31 are its 32 cells.
             // Wave w steps h only after wave w-1 finished step h-1 (its column cl-1 results) and
-            // at most RR-4 steps ahead of wave w+1 (ring slots).  ST_TWIN: lane L + 32 is the twin
+            // at most RR-4 steps ahead of wave w+1 (ring slots).  TWIN: lane L + 32 is the twin
             // of cell lane L -- same cell, same candidate mask; L evaluates the cell's 1st, 3rd, ...
             // candidate and L + 32 its 2nd, 4th, ..., handed back with one v_permlane32_swap.
             const int w = wave;
@@ -455,7 +484,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
 #endif
                 const int a = h - bl - cl;
                 const bool act = col && a >= 0 && a < P.A;
-                const bool actx = (ST_TWIN ? colx : col) && a >= 0 && a < P.A;   // the lanes that evaluate
+                const bool actx = (TWIN ? colx : col) && a >= 0 && a < P.A;   // the lanes that evaluate
                 // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
                 unsigned long long tw0 = 0;
                 for (;;) {
@@ -550,7 +579,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     for (int i_ = 0; i_ < ST_VALU_PROBE; ++i_) asm volatile("v_add_u32 %0, %0, 1" : "+v"(x_));
                 }
 #endif
-#if ST_TWIN
+                bool twin_done = false;   // wave-uniform
+                if constexpr (TWIN) {
                 // ---- candidates in pairs: the cell lane takes the lowest remaining one, its twin
                 //      the next; one ptd per lane per pass, applied in the reference check order
                 //      (strict '<', first minimum wins: cpu_lib/makelevelset3.cpp:94-99, 143-149) ----
@@ -565,6 +595,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
 #endif
                 // at most 2 candidates per cell (else the wave-wide compaction below balances them)
                 if (__all(__popc(fmask) <= 2u)) {
+                    twin_done = true;
                     const f3 gx = st_gx(P, a, b, c);
                     unsigned fm = cell_lane ? fmask : (fmask & (fmask - 1u));
                     if (__any(fm != 0u)) {
@@ -598,15 +629,19 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                         win = take2 ? e2 : win;
                     }
                 } else {
-                fmask = cell_lane ? fmask : 0u;   // the compaction below lists each cell's pairs once
-#endif
+                    fmask = cell_lane ? fmask : 0u;   // the compaction below lists each cell's pairs once
+                }
+                }
+                if (!twin_done) {
                 // ---- at most one candidate per cell (the common case away from the surface):
                 //      each cell lane evaluates its own, no compaction and no LDS exchange ----
                 const bool single = __all(__popc(fmask) <= 1);
-#if defined(ST_STEP_PROF) && !ST_TWIN
-                { const unsigned long long t_ = clock64(); sp_c[1] += t_ - sp_t; sp_t = t_; }
-                if (single) ++sp_n[__any(fmask != 0u) ? 1 : 0];
-                else ++sp_n[2];
+#ifdef ST_STEP_PROF
+                if constexpr (!TWIN) {
+                    { const unsigned long long t_ = clock64(); sp_c[1] += t_ - sp_t; sp_t = t_; }
+                    if (single) ++sp_n[__any(fmask != 0u) ? 1 : 0];
+                    else ++sp_n[2];
+                }
 #endif
                 if (single) {
                     if (fmask) {
@@ -664,8 +699,8 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
-#if defined(ST_STEP_PROF) && !ST_TWIN
-                sp_n[3] += (unsigned long long)total;
+#ifdef ST_STEP_PROF
+                if constexpr (!TWIN) sp_n[3] += (unsigned long long)total;
 #endif
                 // ---- apply in the reference check order: strict '<', first minimum wins ----
                 if (act) {   // branch-free: all 7 slots read at once, non-candidates masked out
@@ -681,9 +716,7 @@ __global__ void __launch_bounds__(ST_THREADS, ST_WPE_DEF) k_sweep_tile(StParams 
                     }
                 }
                 }
-#if ST_TWIN
-                }
-#endif
+                }   // !twin_done
 #ifdef ST_STEP_PROF
                 { const unsigned long long t_ = clock64(); sp_c[2] += t_ - sp_t; sp_t = t_; }
 #endif
@@ -1003,6 +1036,7 @@ struct TileSweepWorkspace {
     size_t cap_mtasks = 0;
     long long mkey = -1;   // (ni, nj, nk, first sweep, count) of the uploaded graph
     double chain_steps = 0.0;   // modelled critical path of that graph, in steps
+    bool thr = false;           // the last multi-sweep launch ran the throughput configuration
     unsigned mepoch = 0;
 };
 
@@ -1079,6 +1113,26 @@ inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int
     return 0;
 }
 
+// Launch k_sweep_tile with the configuration `thr` selects (st_use_thr), its lead cap applied.
+template <bool SLAB, bool TRACE, bool MULTI>
+inline void st_launch(bool thr, int grid, hipStream_t st, StParams &P, int lead_override)
+{
+    const int lead = thr ? StCfgThr::LEAD : StCfgLat::LEAD;
+    P.lead = (lead_override >= 0 && lead_override < lead) ? lead_override : lead;
+    if (getenv("SDFGEN_OCC")) {   // diagnostics: resident workgroups per CU
+        const void *f = thr ? (const void *)k_sweep_tile<StCfgThr, SLAB, TRACE, MULTI>
+                            : (const void *)k_sweep_tile<StCfgLat, SLAB, TRACE, MULTI>;
+        int occ = -1;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, thr ? StCfgThr::THREADS : StCfgLat::THREADS, 0);
+        hipFuncAttributes fa;
+        (void)hipFuncGetAttributes(&fa, f);
+        fprintf(stderr, "k_sweep_tile<%s>: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", thr ? "thr" : "lat", occ,
+                fa.numRegs, fa.sharedSizeBytes, fa.localSizeBytes);
+    }
+    if (thr) hipLaunchKernelGGL((k_sweep_tile<StCfgThr, SLAB, TRACE, MULTI>), dim3(grid), dim3(StCfgThr::THREADS), 0, st, P);
+    else hipLaunchKernelGGL((k_sweep_tile<StCfgLat, SLAB, TRACE, MULTI>), dim3(grid), dim3(StCfgLat::THREADS), 0, st, P);
+}
+
 // Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long *cell,
                       const float origin[3], float dx, int ni, int nj, int nk, int di, int dj,
@@ -1141,7 +1195,6 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
             }
         }
     }
-    P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
     P.clo = W.clo;
     P.chi = W.chi;
     P.ntri = W.ntri;
@@ -1153,17 +1206,10 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
-    if (getenv("SDFGEN_OCC")) {   // diagnostics: resident workgroups per CU
-        int occ = -1;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_sweep_tile<false, false>, ST_THREADS, 0);
-        hipFuncAttributes fa;
-        (void)hipFuncGetAttributes(&fa, (const void *)k_sweep_tile<false, false>);
-        fprintf(stderr, "k_sweep_tile: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", occ, fa.numRegs,
-                fa.sharedSizeBytes, fa.localSizeBytes);
-    }
-    if (slab.on) hipLaunchKernelGGL((k_sweep_tile<true, false>), dim3(grid), dim3(ST_THREADS), 0, st, P);
-    else if (P.trace) hipLaunchKernelGGL((k_sweep_tile<false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
-    else hipLaunchKernelGGL((k_sweep_tile<false, false>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    const bool thr = st_use_thr(ntasks);
+    if (slab.on) st_launch<true, false, false>(thr, grid, st, P, W.lead_override);
+    else if (P.trace) st_launch<false, true, false>(thr, grid, st, P, W.lead_override);
+    else st_launch<false, false, false>(thr, grid, st, P, W.lead_override);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }
@@ -1408,7 +1454,6 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     P.nJ = nJ;
     P.nK = nKq[me];
     P.ntasks = ntasks;
-    P.lead = (W.lead_override >= 0 && W.lead_override < ST_LEAD) ? W.lead_override : ST_LEAD;
     P.cs = cs[me];
     P.ce = ce[me];
     P.hbC = ce[me] - cs[me];
@@ -1452,8 +1497,12 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
-    if (nsl > 1) hipLaunchKernelGGL((k_sweep_tile<true, false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
-    else hipLaunchKernelGGL((k_sweep_tile<false, false, true>), dim3(grid), dim3(ST_THREADS), 0, st, P);
+    // configuration by this slab's tiles per sweep (the largest sweep of the launch)
+    int tiles = 0;
+    for (int q = 0; q < ns; ++q) tiles = std::max(tiles, nJ * nKq[(size_t)q * nsl + me]);
+    W.thr = st_use_thr(tiles);
+    if (nsl > 1) st_launch<true, false, true>(W.thr, grid, st, P, W.lead_override);
+    else st_launch<false, false, true>(W.thr, grid, st, P, W.lead_override);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }

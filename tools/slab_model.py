@@ -1,0 +1,141 @@
+"""Per-phase model of the Z-slab run over N GPUs: predicts the C3 / C4 times and the
+1 -> N strong-scaling efficiency from measured single-GPU quantities, before an 8-GPU node exists.
+
+    python tools/slab_model.py            (the measured inputs are in INPUTS, with their sources)
+
+Phases of one call on N slabs (every slab runs them at once; the call takes the slowest slab):
+  local    prep + band + sign: no exchange, work divides by N           t_local(1) / N
+  first    the one-launch first pass (sweeps 1-8): the larger of
+             chain   chain_steps(N) * s_iso + 8 * (N - 1) * h_x   -- the wavefront's critical path
+                     (tile steps of the task graph over ALL slabs, chain_model below) times the
+                     isolated tile step, plus one cross-GPU hop per slab boundary per sweep
+             work    T_first_work / N                              -- the tiles' throughput
+           times a crowding factor: at one GPU the measured first pass lies above both bounds
+           (C3: the loaded step is 1.7x the isolated one -- tiles on the critical path share CUs with
+           the others); crowd(1) = measured / max(chain, work), and a slab of 1/N of the tiles crowds
+           its GPU 1/N as much: crowd(N) = 1 + (crowd(1) - 1) / N
+  second   sweeps 9-16, each: Jacobi scan + list (work, / N) + the repair chains (a few dozen
+           dependent relabels; they do not shorten with N) + the neighbour handshakes
+           (DONE/READY flags: 2 * h_flag per sweep) + one cross-slab hand-off per boundary a
+           chain crosses (inbound ring: (N - 1) * h_x at most)
+Inputs are measured on one MI355X (bench line, rocprof, tools/uc_lat): see INPUTS.  h_x, the cross-GPU
+granule latency over xGMI, cannot be measured on a one-GPU box: 2 us is assumed (the on-chip
+uncached system-scope round trip is 0.82 us, tools/uc_lat).
+"""
+import json
+
+# ---- measured inputs (one MI355X, round 3) ----
+INPUTS = {
+    "c3_sphere1m_256": {   # bench r03c: 18.52 ms total; tile launch 13.87 ms; 8 sparse sweeps 3.55 ms
+        "dims": (256, 256, 256), "t_local": 0.8650, "t_first": 13.866, "t_second": 3.5525,
+        "t_repair_per_sweep": 0.280,   # k_sp_recheck avg at C3 (rocprof r03b), the chain part of a sweep
+        "t_first_work": 5.6,           # tile work at full throughput: C4's 45.0 ms x 1/8 of the cells
+    },
+    "c4_sphere1m_512": {   # bench r03c zslab_c4 side object: 64.74 ms; tile 45.0 ms; sparse 17.5 ms
+        "dims": (512, 512, 512), "t_local": 1.9414, "t_first": 45.001, "t_second": 17.5045,
+        "t_repair_per_sweep": 0.62,    # repair_ms per sweep, 2-slab rehearsal (r03c_n2 zslab_c4), median
+        "t_first_work": 45.0,          # throughput-bound at one GPU: the launch itself
+    },
+}
+S_ISO_US = 1.559     # isolated tile step (bench latency probe, 1024x9x9 grid)
+H_X_US = 2.0         # cross-GPU granule hand-off over xGMI (assumed; on-chip uncached round trip 0.82 us)
+H_FLAG_US = 2.0      # one DONE / READY flag hand-off between neighbour GPUs (assumed, as h_x)
+ST_T = 8
+DIRS = [(+1, +1, +1), (-1, -1, -1), (+1, +1, -1), (-1, -1, +1), (+1, -1, +1), (-1, +1, -1), (+1, -1, -1), (-1, +1, +1)]
+
+
+def _c_range(kb, ke, nk, dk):
+    if dk > 0:
+        return max(kb, 1) - 1, ke - 1
+    return nk - 1 - min(ke, nk - 1), nk - 1 - kb
+
+
+def _tile_phys(T, c0, c1, n, d):
+    xl, xh = c0 + ST_T * T, min(c0 + ST_T * T + ST_T, c1) - 1
+    return (xl + 1, xh + 1) if d > 0 else (n - 2 - xh, n - 2 - xl)
+
+
+def _covering(lo, hi, c0, c1, n, d):
+    xl, xh = (lo - 1, hi - 1) if d > 0 else (n - 2 - hi, n - 2 - lo)
+    xl, xh = max(xl, c0), min(xh, c1 - 1)
+    if xl > xh:
+        return None
+    return (xl - c0) // ST_T, (xh - c0) // ST_T
+
+
+def chain_model(ni, nj, nk, nslabs):
+    """tile_sweep_multi's schedule model (sweep_tile.hpp) for all slabs: the critical path of the
+    first-pass launch in tile steps.  Estimated starts: +1 hop per upstream tile of the same sweep
+    (across slab boundaries too), + one tile duration after each previous-sweep tile it waits for."""
+    A, B = ni - 1, nj - 1
+    nJ = (B + ST_T - 1) // ST_T
+    kb = [r * nk // nslabs for r in range(nslabs + 1)]
+    wc = (A + 2.0 * (ST_T - 1)) / ST_T
+    cs, ce, nK = {}, {}, {}
+    for q in range(8):
+        for r in range(nslabs):
+            cs[q, r], ce[q, r] = _c_range(kb[r], kb[r + 1], nk, DIRS[q][2])
+            nK[q, r] = max(0, (ce[q, r] - cs[q, r] + ST_T - 1) // ST_T)
+    kv = {}
+    for q in range(8):
+        d, dp = DIRS[q], DIRS[(q + 7) % 8]
+        for rr in range(nslabs):
+            r = rr if d[2] > 0 else nslabs - 1 - rr
+            ru = r - 1 if d[2] > 0 else r + 1
+            for J in range(nJ):
+                for K in range(nK[q, r]):
+                    v = 0.0
+                    if J:
+                        v = max(v, kv[q, r, J - 1, K] + 1.0)
+                    if K:
+                        v = max(v, kv[q, r, J, K - 1] + 1.0)
+                    elif 0 <= ru < nslabs and nK[q, ru] > 0:
+                        v = max(v, kv[q, ru, J, nK[q, ru] - 1] + 1.0)
+                    if q:
+                        jl, jh = _tile_phys(J, 0, B, nj, d[1])
+                        kl, kh = _tile_phys(K, cs[q, r], ce[q, r], nk, d[2])
+                        cj = _covering(jl - 1, jh + 1, 0, B, nj, dp[1])
+                        ck = _covering(kl - 1, kh + 1, cs[q - 1, r], ce[q - 1, r], nk, dp[2])
+                        if cj and ck:
+                            for J2 in range(cj[0], cj[1] + 1):
+                                for K2 in range(ck[0], ck[1] + 1):
+                                    v = max(v, kv[q - 1, r, J2, K2] + wc)
+                    kv[q, r, J, K] = v
+    return (max(kv.values()) + wc) * ST_T
+
+
+def predict(name, inp, ns=(1, 2, 4, 8)):
+    ni, nj, nk = inp["dims"]
+    c1 = chain_model(ni, nj, nk, 1)
+    chain1 = c1 * S_ISO_US * 1e-3
+    crowd = inp["t_first"] / max(chain1, inp["t_first_work"])   # >= 1: sharing CUs with other tiles
+    t_scan = inp["t_second"] / 8 - inp["t_repair_per_sweep"]     # Jacobi scan + list + launch gaps per sweep
+    rows = []
+    for n in ns:
+        cn = chain_model(ni, nj, nk, n) if n > 1 else c1
+        chain = cn * S_ISO_US * 1e-3 + 8 * (n - 1) * H_X_US * 1e-3
+        work = inp["t_first_work"] / n
+        first = max(chain, work) * (1.0 + (crowd - 1.0) / n)
+        second = 8 * (t_scan / n + inp["t_repair_per_sweep"] + (2 * H_FLAG_US + (n - 1) * H_X_US) * 1e-3 * (n > 1))
+        local = inp["t_local"] / n
+        total = local + first + second
+        rows.append({"n": n, "chain_steps": round(cn, 1), "first_chain_ms": round(chain, 3),
+                     "first_work_ms": round(work, 3), "first_ms": round(first, 3), "second_ms": round(second, 3),
+                     "local_ms": round(local, 3), "total_ms": round(total, 3)})
+    t1 = rows[0]["total_ms"]
+    for r in rows:
+        r["efficiency"] = round(t1 / (r["n"] * r["total_ms"]), 3)
+    return {"workload": name, "crowd_factor_1gpu": round(crowd, 3), "inputs": inp, "s_iso_us": S_ISO_US,
+            "h_x_us": H_X_US, "rows": rows}
+
+
+def main():
+    for name, inp in INPUTS.items():
+        res = predict(name, inp)
+        print(json.dumps({k: v for k, v in res.items() if k != "rows"}))
+        for r in res["rows"]:
+            print("  ", json.dumps(r))
+
+
+if __name__ == "__main__":
+    main()
