@@ -10,8 +10,8 @@
 //              ascending-t strict-< rule; ray-parity counts (:203-236)
 //   sweeps   : 2 passes x 8 directions of the Gauss-Seidel sweep (:238-292),
 //              reproduced bit-exactly by a hyperplane-ordered wavefront
-//   k_sign   : one wave per (j,k) row -- ballot prefix parity, sign flip, output in
-//              the caller's layout (:294-303)
+//   k_sign   : one wave per (j,k) row -- ballot prefix parity, sign flip, i-fastest output
+//              (:294-303); k_sign_kfast the same through an LDS tile for k-fastest output
 // Cell state is one u64 per cell: high word = phi bits, low word = closest_tri.
 // Line references are to /root/reference/cpu_lib/makelevelset3.cpp unless noted.
 #include <hip/hip_runtime.h>
@@ -407,6 +407,51 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
 }
 
 // Diagnostics kernels.
+// The sign pass with k-fastest output (SDFGEN_LAYOUT_KFAST: numpy (ni,nj,nk) C-order, the .sdf body):
+// k_sign's row walk along i would write every lane to its own line (stride nj*nk floats) -- 3.7 ms
+// at 512^3 against 0.4 for i-fastest.  Here a workgroup owns 64 rows (j, k0..k0+63) and walks i in
+// chunks of 64: each wave signs 16 of the rows (prefix parity along i by ballot, carries kept per
+// row) into an LDS tile [k][i], then the tile is written transposed -- for each i, 64 consecutive k:
+// one 256-byte run per wave store.
+__global__ void __launch_bounds__(256) k_sign_kfast(const u64 *__restrict__ cell, const uint32_t *__restrict__ cnt,
+                                                    Grid g, float *__restrict__ out, int k_lo, int k_cnt)
+{
+    __shared__ float s_t[64][65];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int kblocks = (k_cnt + 63) / 64;
+    const uint64_t ntile = (uint64_t)g.nj * kblocks;
+    const u64 below = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);   // lanes 0..lane
+    for (uint64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        const int j = (int)(tile % g.nj), kb = (int)(tile / g.nj) * 64;
+        uint32_t carry[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) carry[r] = 0;
+        for (int i0 = 0; i0 < g.ni; i0 += 64) {
+            const int i = i0 + lane;
+            const bool ok = i < g.ni;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {   // rows kb + 16 w + r (wave-uniform)
+                const int kr = kb + 16 * w + r;
+                if (kr < k_cnt) {
+                    const size_t base = cidx(0, j, k_lo + kr, g.ni, g.nj);
+                    const uint32_t par = ok ? (cnt[base + i] & 1u) : 0u;
+                    const u64 mask = __ballot(par);
+                    const uint32_t pre = (carry[r] + (uint32_t)__popcll(mask & below)) & 1u;
+                    uint32_t bits = ok ? (uint32_t)(cell[base + i] >> 32) : 0u;
+                    if (pre) bits ^= 0x80000000u;
+                    s_t[16 * w + r][lane] = __uint_as_float(bits);
+                    carry[r] = (carry[r] + (uint32_t)__popcll(mask)) & 1u;
+                }
+            }
+            __syncthreads();
+            const int kk = kb + lane;
+            for (int ii = w; ii < 64 && i0 + ii < g.ni; ii += 4)
+                if (kk < k_cnt) out[((size_t)(i0 + ii) * g.nj + j) * k_cnt + kk] = s_t[lane][ii];
+            __syncthreads();
+        }
+    }
+}
+
 __global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__restrict__ out, int variant)
 {
     uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -625,6 +670,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->wf.count = getenv("SDFGEN_COUNT_EVALS") != nullptr;
         const char *tr = getenv("SDFGEN_TRACE_SWEEP");   // diagnostics: per-task timing of one sweep
         ws->wf.trace_sweep = tr ? atoi(tr) : -1;
+        ws->wf.trace_multi = getenv("SDFGEN_TRACE_MULTI") != nullptr;   // diagnostics: the whole first pass
         const char *gr = getenv("SDFGEN_TILE_GRID");     // diagnostics: cap on resident workgroups
         ws->wf.grid_override = gr ? atoi(gr) : 0;
         const char *ld = getenv("SDFGEN_TILE_LEAD");      // diagnostics: inter-wave lead
@@ -721,8 +767,12 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipEventRecord(ev[19], st));
     {
         const uint64_t rows = (uint64_t)nj * nk;
-        hipLaunchKernelGGL(k_sign, dim3(grid_for(rows * 64, 256, 65536)), dim3(256), 0, st, ws->cell, ws->cnt, g,
-                           layout, d_out, 0, nk);
+        if (layout == SDFGEN_LAYOUT_KFAST)
+            hipLaunchKernelGGL(k_sign_kfast, dim3(grid_for((uint64_t)nj * ((nk + 63) / 64), 1, 65536)), dim3(256), 0, st,
+                               ws->cell, ws->cnt, g, d_out, 0, nk);
+        else
+            hipLaunchKernelGGL(k_sign, dim3(grid_for(rows * 64, 256, 65536)), dim3(256), 0, st, ws->cell, ws->cnt, g,
+                               layout, d_out, 0, nk);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[20], st));
@@ -773,6 +823,9 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
                         "cycles/step poll %.0f mask %.0f eval %.0f writeback %.0f\n", steps, wf_stats[8] / steps,
                 wf_stats[9] / steps, wf_stats[10] / steps, wf_stats[10] ? (double)wf_stats[11] / wf_stats[10] : 0.0,
                 wf_stats[4] / steps, wf_stats[5] / steps, wf_stats[6] / steps, wf_stats[7] / steps);
+        fprintf(stderr, "step profile: eval cycles per step of the twin path %.0f (%.0f steps), of the compaction path %.0f "
+                        "(%.0f steps)\n", wf_stats[12] / std::max(1.0, (double)wf_stats[9]), (double)wf_stats[9],
+                wf_stats[13] / std::max(1.0, (double)wf_stats[10]), (double)wf_stats[10]);
     }
 #endif
     p.sweep_evals = wf_stats[0];
@@ -887,10 +940,11 @@ int slab_preload_kernels(Err &err)
 {
     if (getenv("SDFGEN_NO_KERNEL_PRELOAD")) return 0;   // diagnostics
     const void *k[] = {(const void *)k_prep_soup, (const void *)k_init, (const void *)k_band_lds,
-                       (const void *)k_sign, (const void *)k_sweep_tile<StCfgLat, true, false, false>,
+                       (const void *)k_sign, (const void *)k_sign_kfast, (const void *)k_sweep_tile<StCfgLat, true, false, false>,
                        (const void *)k_sweep_tile<StCfgLat, true, false, true>,
                        (const void *)k_sweep_tile<StCfgThr, true, false, false>,
                        (const void *)k_sweep_tile<StCfgThr, true, false, true>, (const void *)k_sp_jacobi<true>,
+                       (const void *)k_sp_jacobi_t<true>,
                        (const void *)k_sp_jlist<true>, (const void *)k_sp_recheck<true>, (const void *)k_sp_slab_wait,
                        (const void *)k_sp_slab_halo, (const void *)k_sp_slab_export};
     for (const void *f : k) {
@@ -1036,7 +1090,7 @@ int slab_prepare(SlabSession *S, uint64_t ntri, Err &err)
             return rc;
     }
     if (slab_sparse_on(S)) {
-        if (int rc = sp_reserve(S->sp, plane_cells * kc, st))
+        if (int rc = sp_reserve(S->sp, plane_cells * kc, ni, nj, st))
             return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse buffers");
         if (!S->alt_mem) {
             HIPCHK(hipMalloc((void **)&S->alt_mem, plane_cells * kc * sizeof(u64)));
@@ -1215,8 +1269,12 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     HIPCHK(hipEventRecord(ev[19], st));
     {
         const uint64_t rows = (uint64_t)nj * kc;
-        hipLaunchKernelGGL(k_sign, dim3(grid_for(rows * 64, 256, 65536)), dim3(256), 0, st, cur, S->cnt, g,
-                           layout, d_out, S->k_begin, kc);
+        if (layout == SDFGEN_LAYOUT_KFAST)
+            hipLaunchKernelGGL(k_sign_kfast, dim3(grid_for((uint64_t)nj * ((kc + 63) / 64), 1, 65536)), dim3(256), 0, st,
+                               cur, S->cnt, g, d_out, S->k_begin, kc);
+        else
+            hipLaunchKernelGGL(k_sign, dim3(grid_for(rows * 64, 256, 65536)), dim3(256), 0, st, cur, S->cnt, g,
+                               layout, d_out, S->k_begin, kc);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[20], st));

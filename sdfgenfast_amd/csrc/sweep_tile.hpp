@@ -320,6 +320,10 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         __syncthreads();
         const int task = s_task;
         if (task >= P.ntasks) break;
+        // TRACE + MULTI (tools/trace_multi.py): [0] setup done, [1] step 0 done, [2] first b-edge halo
+        // entries (from tile J - 1) landed, [3] end, [4] first own entries landed, [5] step 8 done, [6] sweep slot << 32 | J << 16 | K,
+        // [7] claim time
+        const unsigned long long t_claim = (TRACE && MULTI && P.trace) ? wall_clock64() : 0ull;
         int J, K;
         if (MULTI) {
             const int4 tk = P0.mtasks[task];
@@ -476,7 +480,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             unsigned polls = 0;
             unsigned long long t_wait = 0, w_own = 0, w_halo = 0, t_comp = 0, c_comp = 0;   // trace-only
 #ifdef ST_STEP_PROF   // diagnostics: where a compute step's cycles go (host prints the sums)
-            unsigned long long sp_c[4] = {0, 0, 0, 0}, sp_n[4] = {0, 0, 0, 0}, sp_t = 0;
+            unsigned long long sp_c[4] = {0, 0, 0, 0}, sp_n[4] = {0, 0, 0, 0}, sp_t = 0, sp_ev[2] = {0, 0};
 #endif
             for (int h = 0; h < nsteps; ++h) {
 #ifdef ST_STEP_PROF
@@ -718,7 +722,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 }
                 }   // !twin_done
 #ifdef ST_STEP_PROF
-                { const unsigned long long t_ = clock64(); sp_c[2] += t_ - sp_t; sp_t = t_; }
+                { const unsigned long long t_ = clock64(); sp_c[2] += t_ - sp_t; sp_ev[twin_done ? 0 : 1] += t_ - sp_t; sp_t = t_; }
 #endif
                 if (act) {
                     const int src = win < 0 ? e_own : win;
@@ -751,22 +755,31 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #ifdef ST_STEP_PROF
                 sp_c[3] += clock64() - sp_t;
 #endif
-                if (TRACE && P.trace && w == 0 && L == 0 && (h == 0 || h == nsteps / 2))
-                    P.trace[8 * task + (h == 0 ? 1 : 2)] = wall_clock64();
+                if (TRACE && P.trace && w == 0 && L == 0 && (h == 0 || h == (MULTI ? 8 : nsteps / 2)))
+                    P.trace[8 * task + (h == 0 ? 1 : (MULTI ? 5 : 2))] = wall_clock64();   // MULTI: [5] = step 8 done
             }
             __builtin_amdgcn_s_setprio(0);
 #ifdef ST_STEP_PROF
             if (P.stats && L == 0) {
                 for (int i_ = 0; i_ < 4; ++i_) atomicAdd(P.stats + 4 + i_, sp_c[i_]);
                 for (int i_ = 0; i_ < 4; ++i_) atomicAdd(P.stats + 8 + i_, sp_n[i_]);
+                atomicAdd(P.stats + 12, sp_ev[0]);
+                atomicAdd(P.stats + 13, sp_ev[1]);
             }
 #endif
             if (TRACE && P.trace && w == 0 && L == 0) {
                 P.trace[8 * task + 3] = wall_clock64();
-                P.trace[8 * task + 4] = t_wait;
-                P.trace[8 * task + 5] = w_own + (w_halo << 32);
-                P.trace[8 * task + 6] = c_comp;
-                P.trace[8 * task + 7] = t_comp;
+                if (!MULTI) {
+                    P.trace[8 * task + 4] = t_wait;
+                    P.trace[8 * task + 5] = w_own + (w_halo << 32);
+                }
+                if (MULTI) {
+                    P.trace[8 * task + 6] = ((unsigned long long)P0.mtasks[task].z << 32) | ((unsigned)J << 16) | (unsigned)K;
+                    P.trace[8 * task + 7] = t_claim;
+                } else {
+                    P.trace[8 * task + 6] = c_comp;
+                    P.trace[8 * task + 7] = t_comp;
+                }
             }
         } else {
             const int bl = L & (ST_T - 1), cl = L >> 3;   // helper lane L prefetches column (bl, cl)
@@ -822,6 +835,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             static_assert(ST_G == 4 || ST_G == 2, "helper pipeline is written out for 2- or 4-element batches");
             unsigned idle = 0;
             unsigned long long t_idle = 0;   // Z-slab: wall ticks this helper spent backing off (TM_*)
+            bool tr_halo = false, tr_own = false;   // TRACE + MULTI: first landings recorded
             for (;;) {
                 // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
                 // may finish step h while wave w-1 is still on step h (it needs only h-1 of it).
@@ -960,6 +974,13 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 lds_drain();
                 if (L == 0 && gA) lds_st(&s_hdr[0], fB);
                 if (hvalid && hp) lds_st(&s_halo_ready[L], hB);
+                if (TRACE && MULTI && P.trace) {   // [2] first halo entries landed, [4] first own entries landed
+                    const bool h_now = __any(hvalid && hp > 0 && L < ST_T), o_now = gA > 0;   // b-edge streams (from J - 1)
+                    if (h_now && !tr_halo && L == 0) P.trace[8 * task + 2] = wall_clock64();
+                    if (o_now && !tr_own && L == 0) P.trace[8 * task + 4] = wall_clock64();
+                    tr_halo |= h_now;
+                    tr_own |= o_now;
+                }
                 const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
                 fA = fB; gA = gB; hA = hB; hcA = hcB;
                 c0 = n0; c1 = n1; c2 = n2; c3 = n3;
@@ -1010,6 +1031,7 @@ struct TileSweepWorkspace {
     unsigned long long *hb = nullptr, *hc = nullptr, *stats = nullptr, *trace = nullptr;
     size_t cap_trace = 0;
     int trace_sweep = -1;      // which sweep (0..15) to trace, -1 = none
+    bool trace_multi = false;  // trace every task of the one-launch first pass (diagnostics)
     int cur_sweep = 0;
     int grid_override = 0;     // diagnostics: cap on resident workgroups
     int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
@@ -1502,7 +1524,11 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     for (int q = 0; q < ns; ++q) tiles = std::max(tiles, nJ * nKq[(size_t)q * nsl + me]);
     W.thr = st_use_thr(tiles);
     if (nsl > 1) st_launch<true, false, true>(W.thr, grid, st, P, W.lead_override);
-    else st_launch<false, false, true>(W.thr, grid, st, P, W.lead_override);
+    else if (W.trace_multi) {   // diagnostics: per-task timeline of the whole launch (tools/trace_multi.py)
+        if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(-5, "trace");
+        P.trace = W.trace;
+        st_launch<false, true, true>(W.thr, grid, st, P, W.lead_override);
+    } else st_launch<false, false, true>(W.thr, grid, st, P, W.lead_override);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }
