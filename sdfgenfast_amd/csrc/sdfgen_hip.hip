@@ -944,7 +944,6 @@ int slab_preload_kernels(Err &err)
                        (const void *)k_sweep_tile<StCfgLat, true, false, true>,
                        (const void *)k_sweep_tile<StCfgThr, true, false, false>,
                        (const void *)k_sweep_tile<StCfgThr, true, false, true>, (const void *)k_sp_jacobi<true>,
-                       (const void *)k_sp_jacobi_t<true>,
                        (const void *)k_sp_jlist<true>, (const void *)k_sp_recheck<true>, (const void *)k_sp_slab_wait,
                        (const void *)k_sp_slab_halo, (const void *)k_sp_slab_export};
     for (const void *f : k) {
@@ -1090,7 +1089,7 @@ int slab_prepare(SlabSession *S, uint64_t ntri, Err &err)
             return rc;
     }
     if (slab_sparse_on(S)) {
-        if (int rc = sp_reserve(S->sp, plane_cells * kc, ni, nj, st))
+        if (int rc = sp_reserve(S->sp, plane_cells * kc, st))
             return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse buffers");
         if (!S->alt_mem) {
             HIPCHK(hipMalloc((void **)&S->alt_mem, plane_cells * kc * sizeof(u64)));

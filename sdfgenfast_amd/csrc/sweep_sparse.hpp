@@ -576,130 +576,6 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
     if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
 }
 
-// k_sp_jacobi as a tiled stream (default; SDFGEN_JACOBI_TILED=0 for the flat scan above): a
-// workgroup owns 64 i x 4 j rows and walks JT_K planes in the sweep's k direction.  Each cell's 7
-// upwind low words come from LDS -- the tile's rows of this plane and of the previous one (kept from
-// the last step), a j-halo row and the i-halo words -- so a cell costs ONE global load (its own
-// state) instead of eight; the flat scan was load-issue-bound (512^3: 0.88 ms per sweep, 2.4 TB/s).
-// Same decisions, same list, same copies: only where the words come from differs.
-constexpr int JT_I = 64, JT_J = 4, JT_K = 16;
-struct JtGeom {
-    int nI, nJ, nK, planes;   // tiles along i, j, k; the launch's planes (k_hi - k_lo)
-    unsigned long long ntiles;
-};
-__host__ __device__ inline JtGeom jt_geom(int ni, int nj, int k_lo, int k_hi)
-{
-    JtGeom g;
-    g.planes = k_hi - k_lo;
-    g.nI = (ni + JT_I - 1) / JT_I;
-    g.nJ = (nj + JT_J - 1) / JT_J;
-    g.nK = (g.planes + JT_K - 1) / JT_K;
-    g.ntiles = (unsigned long long)g.nI * g.nJ * g.nK;
-    return g;
-}
-
-template <bool SLAB>
-__global__ void __launch_bounds__(256) k_sp_jacobi_t(SpParams P)
-{
-    // [plane parity][row: 0 = the j-halo row, 1..4 the tile's rows in the sweep's j order][1 + i - i0]
-    __shared__ uint32_t s_w[2][JT_J + 1][JT_I + 2];
-    __shared__ unsigned s_list[4][SP_JWAVE];
-    const JtGeom G = jt_geom(P.ni, P.nj, P.k_lo, P.k_hi);
-    // XCD-aware: blocks are dealt round-robin to the 8 XCDs; XCD x takes the x-th contiguous eighth
-    // of the tiles (i fastest, then j, then k), so the halo rows a tile reads sit in its own L2
-    const unsigned long long b = blockIdx.x;
-    const unsigned long long t = G.ntiles % 8 == 0 ? (b % 8) * (G.ntiles / 8) + b / 8 : b;
-    if (t >= G.ntiles) return;
-    const int ti = (int)(t % G.nI), tj = (int)((t / G.nI) % G.nJ), tk = (int)(t / ((unsigned long long)G.nI * G.nJ));
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = w + 1;
-    const int i0 = ti * JT_I, j0 = tj * JT_J;
-    const int i = i0 + lane;
-    // rows in the sweep's j order: row r's j - dj neighbour is row r - 1 (row 0: the halo row)
-    const int j = P.dj > 0 ? j0 + w : j0 + JT_J - 1 - w;
-    const int jh = P.dj > 0 ? j0 - 1 : j0 + JT_J;   // halo row
-    const int ie = P.di > 0 ? i0 - 1 : i0 + JT_I;   // i-halo word of each row (the i - di of the edge lane)
-    const int xe = P.di > 0 ? 0 : JT_I + 1;
-    const int x0 = lane + 1 - P.di;                 // LDS index of (i - di)
-    // planes of this tile in the sweep's k direction
-    const int pa = tk * JT_K, pb = min(G.planes, pa + JT_K);
-    const int kfirst = P.dk > 0 ? P.k_lo + pa : P.k_hi - 1 - pa;
-    const int np = pb - pa;
-    const unsigned part = blockIdx.x % SP_JPARTS;
-    unsigned *buf = s_list[w];
-    unsigned cnt = 0;   // wave-uniform
-    const size_t plane = (size_t)P.ni * P.nj;
-    const bool row_ok = j < P.nj, cell_ok = row_ok && i < P.ni;
-    // low words of row jj of plane k (into s_w[par][row]); words of cells outside the grid are never used
-    auto load_row = [&](int par, int row, int jj, int k, bool from_halo) {
-        uint32_t v = 0, e = 0;
-        if (jj >= 0 && jj < P.nj) {
-            if (from_halo) {   // SLAB: the upstream slab's plane k lives in the halo plane (i + ni*j)
-                const size_t hp = (size_t)P.ni * jj;
-                if (i < P.ni) v = P.hS_up[SDF_CHK(23, hp + i, 0, plane)];
-                if (lane == 0 && ie >= 0 && ie < P.ni) e = P.hS_up[SDF_CHK(23, hp + ie, 0, plane)];
-            } else {
-                const size_t rb = (size_t)P.ni * ((size_t)jj + (size_t)P.nj * k);
-                const uint32_t *L = reinterpret_cast<const uint32_t *>(P.S);
-                if (i < P.ni) v = L[2 * SDF_CHK(22, rb + i, P.c_lo, P.c_lo + P.n)];
-                if (lane == 0 && ie >= 0 && ie < P.ni) e = L[2 * SDF_CHK(22, rb + ie, P.c_lo, P.c_lo + P.n)];
-            }
-        }
-        s_w[par][row][lane + 1] = v;
-        if (lane == 0) s_w[par][row][xe] = e;
-    };
-    int cur = 0;
-    {   // the plane before the first: this slab's own, the upstream slab's halo plane, or none
-        const int kp = kfirst - P.dk;
-        if (kp >= 0 && kp < P.nk) {
-            const bool own = kp >= P.k_lo && kp < P.k_hi;
-            if (own || (SLAB && P.hS_up)) {
-                load_row(1, r, j, kp, !own);
-                if (w == 0) load_row(1, 0, jh, kp, !own);
-            }
-        }
-    }
-    for (int s = 0; s < np; ++s) {
-        const int k = kfirst + s * P.dk;
-        unsigned long long own = 0;
-        const size_t c = (size_t)i + (size_t)P.ni * ((size_t)j + (size_t)P.nj * k);
-        if (cell_ok) own = P.S[SDF_CHK(20, c, P.c_lo, P.c_lo + P.n)];
-        s_w[cur][r][lane + 1] = (uint32_t)own;
-        if (lane == 0) {
-            uint32_t e = 0;
-            if (row_ok && ie >= 0 && ie < P.ni)
-                e = reinterpret_cast<const uint32_t *>(P.S)[2 * SDF_CHK(22, c - lane + (ie - i0), P.c_lo, P.c_lo + P.n)];
-            s_w[cur][r][xe] = e;
-        }
-        if (w == 0) load_row(cur, 0, jh, k, false);
-        __syncthreads();
-        unsigned f = 0;
-        if (cell_ok) {
-            const int pr = cur ^ 1;
-            uint32_t wq[7];
-            wq[0] = s_w[cur][r][x0];
-            wq[1] = s_w[cur][r - 1][lane + 1];
-            wq[2] = s_w[cur][r - 1][x0];
-            wq[3] = s_w[pr][r][lane + 1];
-            wq[4] = s_w[pr][r][x0];
-            wq[5] = s_w[pr][r - 1][lane + 1];
-            wq[6] = s_w[pr][r - 1][x0];
-            int lab[7];
-            if (sp_in(P, i, j, k)) f = sp_mask_w(P, i, j, k, own, wq, lab, false);
-            if (!f) P.X[SDF_CHK(21, c, P.c_lo, P.c_lo + P.n)] = own;
-        }
-        const unsigned long long want = __ballot(f != 0u);
-        if (f) buf[cnt + __builtin_popcountll(want & ((1ull << lane) - 1ull))] = (unsigned)c;
-        cnt += (unsigned)__builtin_popcountll(want);
-        if (cnt > SP_JWAVE - 64) {
-            sp_jlist_flush(P, part, buf, cnt, lane);
-            cnt = 0;
-        }
-        cur ^= 1;
-        __syncthreads();   // the next plane overwrites the buffer read as the previous plane above
-    }
-    if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
-}
-
 // Pass 1b: the listed cells, each exactly as in place (sp_eval against S).
 // Z-slab: it pushes into the neighbours' live halos, so it runs after k_sp_slab_wait saw both
 // neighbours READY.
@@ -1015,13 +891,6 @@ __global__ void __launch_bounds__(256) k_sp_slab_export(SpExportParams E)
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
-// the Jacobi scan: tiled (default) or the flat one (SDFGEN_JACOBI_TILED=0; A/B and tests)
-inline bool sp_jacobi_tiled()
-{
-    const char *e = getenv("SDFGEN_JACOBI_TILED");
-    return !e || atoi(e) != 0;
-}
-
 struct SparseSweepWorkspace {
     int workers = SP_WORKERS_DEFAULT;            // repair-kernel workgroups (diagnostics may lower it)
     unsigned long long ntri = ~0ull;             // soup size for bounds-checked builds
@@ -1051,7 +920,7 @@ inline int sp_grow(T **p, size_t *cap, size_t need, bool zero, hipStream_t st)
 
 // Workspace for sparse sweeps over n cells (allocations only: a Z-slab grows it before it
 // enqueues anything, since a later hipFree would synchronise the device mid-call).
-inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, int ni_, int nj_, hipStream_t st)
+inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, hipStream_t st)
 {
     const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
     if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;
@@ -1064,10 +933,7 @@ inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, int ni_, in
     if (blocks > 16384) blocks = 16384;
     blocks = (blocks + 7) / 8 * 8;
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
-    unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
-    // the tiled scan's bound, as in sp_setup (n cells = this slab's planes)
-    jcap = std::max(jcap, (jt_geom(ni_, nj_, 0, (int)(n / ((unsigned long long)ni_ * nj_))).ntiles + SP_JPARTS - 1) /
-                              SP_JPARTS * (unsigned long long)(JT_I * JT_J * JT_K));
+    const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
     if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
     return 0;
 }
@@ -1096,12 +962,7 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     // it for the ~10 % that are listed would need an in-place fallback whose registers
     // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
-    unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
-    {   // the tiled scan: a part receives at most the cells of its blocks' tiles
-        const int kl = (int)(c_lo / ((unsigned long long)ni * nj)), kh = kl + (int)(n / ((unsigned long long)ni * nj));
-        const JtGeom G = jt_geom(ni, nj, kl, kh);
-        jcap = std::max(jcap, (G.ntiles + SP_JPARTS - 1) / SP_JPARTS * (unsigned long long)(JT_I * JT_J * JT_K));
-    }
+    const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
     if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
     memset(&P, 0, sizeof(P));
     P.soup = soup;
@@ -1156,10 +1017,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, 0, n, P, blocks)) return rc;
     P.S = *cell;
     P.X = W.alt;
-    if (sp_jacobi_tiled())
-        hipLaunchKernelGGL(k_sp_jacobi_t<false>, dim3((unsigned)jt_geom(ni, nj, 0, nk).ntiles), dim3(256), 0, st, P);
-    else
-        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
     if (hipGetLastError() != hipSuccess) return -4;
     const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
     hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
@@ -1248,10 +1106,7 @@ inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const floa
     P.tm_m = L.tm_m;
     const char *stg = getenv("SDFGEN_DEBUG_SPARSE_STAGE");   // diagnostics: stop after kernel n (1 halo .. 4 all)
     const int stage = stg ? atoi(stg) : 4;
-    if (stage >= 2 && sp_jacobi_tiled())
-        hipLaunchKernelGGL(k_sp_jacobi_t<true>, dim3((unsigned)jt_geom(ni, nj, L.k_lo, L.k_hi).ntiles), dim3(256), 0, st, P);
-    else if (stage >= 2)
-        hipLaunchKernelGGL(k_sp_jacobi<true>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    if (stage >= 2) hipLaunchKernelGGL(k_sp_jacobi<true>, dim3((unsigned)blocks), dim3(256), 0, st, P);
     H.word = SP_FL_READY;
     if (stage >= 3) hipLaunchKernelGGL(k_sp_slab_wait, dim3(1), dim3(64), 0, st, H);
     const unsigned long long lblocks = 32 * SP_JPARTS;
