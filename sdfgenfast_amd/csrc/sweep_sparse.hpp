@@ -96,6 +96,10 @@ constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup
 #ifndef SP_IDLE_SLEEP
 #define SP_IDLE_SLEEP 2
 #endif
+#ifndef SP_LOCAL_LANES
+#define SP_LOCAL_LANES 32   // k_sp_recheck: lanes per wave that take no ring tickets (sp_hand_local)
+#endif
+static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least one ring lane");
 
 // the reference's 8 sweep directions in pass order (cpu_lib/makelevelset3.cpp:243-291)
 constexpr int SP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
@@ -367,13 +371,13 @@ __device__ __forceinline__ size_t sp_request_collect(const SpParams &P, int i, i
 // touch 0 while work remains.  (One atomic per lane saturated the word: ~100 returning atomics per
 // microsecond on one address at 256^3 -- DESIGN.md §4.)
 __device__ __forceinline__ void sp_append_wave(const SpParams &P, unsigned shard, unsigned qmask, const size_t (&tgt)[7],
-                                               bool fin)
+                                               bool fin, unsigned nloc = 0)
 {
     const unsigned lane = threadIdx.x & 63;
     const unsigned nq = __popc(qmask);
     const unsigned long long b0 = __ballot(nq & 1u), b1 = __ballot(nq & 2u), b2 = __ballot(nq & 4u),
                              bf = __ballot(fin);
-    if (!(b0 | b1 | b2 | bf)) return;
+    if (!(b0 | b1 | b2 | bf) && nloc == 0u) return;
     const unsigned long long lt = (1ull << lane) - 1ull;
     const unsigned pre = (unsigned)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
     const unsigned long long tot = (unsigned long long)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
@@ -381,7 +385,7 @@ __device__ __forceinline__ void sp_append_wave(const SpParams &P, unsigned shard
     unsigned long long t0 = 0;
     if (lane == 0) {
         // pending += tot - nfin, tail += tot (two's complement in the high half)
-        const unsigned long long old_q = atomicAdd(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE], (tot - nfin) * SP_PENDING_ONE + tot);
+        const unsigned long long old_q = atomicAdd(&P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE], (tot + nloc - nfin) * SP_PENDING_ONE + tot);
         t0 = old_q & 0xffffffffull;
         if (t0 + tot > SP_TAIL_LIMIT) atomicOr(&P.ctl[SP_ERR], 2ull);
     }
@@ -404,13 +408,14 @@ struct SpAppend {
     unsigned qmask;             // this lane's items (slots of tgt)
     bool live;                  // wave-uniform: an atomic is in flight
 };
-__device__ __forceinline__ void sp_append_issue(const SpParams &P, unsigned shard, unsigned qmask, bool fin, SpAppend &A)
+__device__ __forceinline__ void sp_append_issue(const SpParams &P, unsigned shard, unsigned qmask, bool fin,
+                                                unsigned nloc, SpAppend &A)
 {
     const unsigned lane = threadIdx.x & 63;
     const unsigned nq = __popc(qmask);
     const unsigned long long b0 = __ballot(nq & 1u), b1 = __ballot(nq & 2u), b2 = __ballot(nq & 4u),
                              bf = __ballot(fin);
-    A.live = (b0 | b1 | b2 | bf) != 0ull;
+    A.live = (b0 | b1 | b2 | bf) != 0ull || nloc != 0u;
     if (!A.live) return;
     const unsigned long long lt = (1ull << lane) - 1ull;
     A.pre = (unsigned)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
@@ -418,9 +423,10 @@ __device__ __forceinline__ void sp_append_issue(const SpParams &P, unsigned shar
     A.qmask = qmask;
     const unsigned long long nfin = (unsigned long long)__popcll(bf);
     if (lane == 0) {
-        // pending += tot - nfin, tail += tot (two's complement in the high half)
+        // pending += tot + nloc - nfin, tail += tot (two's complement in the high half): the cells
+        // handed to the wave's own lanes (sp_hand_local) run without passing through the ring
         unsigned long long *w = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];
-        const unsigned long long d = (A.tot - nfin) * SP_PENDING_ONE + A.tot;
+        const unsigned long long d = (A.tot + nloc - nfin) * SP_PENDING_ONE + A.tot;
         // (s_nop 1: hipcc pads nothing inside asm -- the operand registers are rewritten right after)
         asm volatile("global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_nop 1" : "=&v"(A.old_q) : "v"(w), "v"(d) : "memory");
     }
@@ -447,6 +453,51 @@ __device__ __forceinline__ void sp_append_finish(const SpParams &P, unsigned sha
 #pragma unroll
     for (int q = 0; q < 7; ++q)
         if ((A.qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + (t++) % P.cap, (unsigned)(tgt[q] + 1));
+}
+
+// wave-synchronous LDS hand-over between lanes of one wave
+__device__ __forceinline__ void sp_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Wave-level (uniform call): the cells the wave's lanes claimed this iteration (qmask / tgt of
+// sp_request_collect) go first to the wave's own idle hand-off lanes (`free_lane`: lanes that take
+// no ring tickets), in (lane, slot) order, through a 64-entry LDS array; only the rest is appended
+// to the ring.  A chain link handed over this way costs no ring round trips (append atomic, slot
+// store, the taker's tail read and slot poll): the taker evaluates it in the next iteration, like a
+// depth-first claim.  Returns the number of cells handed over (wave-uniform); *got = the taken cell.
+__device__ __forceinline__ unsigned sp_hand_local(unsigned *s_hand, unsigned *qmask, const size_t (&tgt)[7],
+                                                  bool free_lane, size_t *got)
+{
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned nq = __popc(*qmask);
+    const unsigned long long fm = __ballot(free_lane), b0 = __ballot(nq & 1u), b1 = __ballot(nq & 2u),
+                             b2 = __ballot(nq & 4u);
+    if (!fm || !(b0 | b1 | b2)) return 0u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    const unsigned tot = (unsigned)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
+    const unsigned nloc = tot < (unsigned)__popcll(fm) ? tot : (unsigned)__popcll(fm);
+    unsigned x = (unsigned)(__popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt));
+    unsigned keep = *qmask;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        if ((*qmask >> q) & 1u) {
+            if (x < nloc) {
+                s_hand[x] = (unsigned)tgt[q];
+                keep &= ~(1u << q);
+            }
+            ++x;
+        }
+    }
+    sp_wave_sync();
+    const unsigned r = (unsigned)__popcll(fm & lt);
+    if (free_lane && r < nloc) *got = s_hand[r];
+    sp_wave_sync();   // every taker has read before the array is written again
+    *qmask = keep;
+    return nloc;
 }
 
 // Pass 1 of the sparse sweep: every cell against the labels of S, in two kernels.
@@ -493,14 +544,6 @@ __device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32, 
         if (SLAB) sp_push(P, i, j, k, c32, (uint32_t)y);
         sp_request_collect(P, i, j, k, c32, false, qmask, tgt);
     }
-}
-
-// wave-synchronous LDS hand-over between lanes of one wave
-__device__ __forceinline__ void sp_wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ void sp_jlist_flush(const SpParams &P, unsigned part, const unsigned *buf, unsigned cnt,
@@ -616,6 +659,7 @@ template <bool SLAB>
 __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 {
     constexpr size_t NONE = ~(size_t)0;
+    __shared__ unsigned s_hand[64];   // sp_hand_local
     unsigned long long runs = 0, claims = 0, h = 0, h_in = 0;
     size_t e = NONE, next = NONE;
     unsigned rq = 1;
@@ -624,6 +668,10 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
     unsigned spins = 0, in_spins = 0;
     const unsigned lane = threadIdx.x & 63;
     const unsigned long long lane_lt = (1ull << lane) - 1ull;
+    // hand-off lanes take work only from their own wave (sp_hand_local), never ring tickets: a
+    // ticket holder is bound to its ring slot.  They leave with the wave once its ring lanes saw the
+    // shard drain (their cells count as pending there, so a drained shard has none running).
+    const bool local = lane >= 64u - (unsigned)SP_LOCAL_LANES;
     const unsigned shard = blockIdx.x & (P.nq - 1u);   // this wave's home work-list shard
     unsigned long long *const q_tail = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];   // pending << 32 | tail
     unsigned long long *const q_head = q_tail + 16;
@@ -645,7 +693,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
         bool fin = false;     // this lane's work item ended this iteration
         {
             // queue tickets for every lane that needs one: ONE atomic on the head word per wave
-            const bool want = !done && e == NONE && !waiting && !(SLAB && in_role);
+            const bool want = !done && e == NONE && !waiting && !(SLAB && in_role) && !local;
             const unsigned long long wm = __ballot(want);
             if (wm) {
                 unsigned long long base = 0;
@@ -698,7 +746,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 in_role = false;
                 atomicAdd(&P.ctl[SP_INDONE], 1ull);
             }
-        } else if (!done && e == NONE) {
+        } else if (!done && e == NONE && !local) {   // a ring lane: its ticket's slot
             // the slot is read only once the tail has passed it (appended; its store may still land)
             const unsigned v = h < (qw & 0xffffffffull) ? sp_ld32(ring + h % P.cap) : 0u;
             if (v) {
@@ -754,19 +802,30 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 sp_order();
             }
         }
+        unsigned nloc = 0;
+        if (SP_LOCAL_LANES) {
+            size_t got = NONE;
+            nloc = sp_hand_local(s_hand, &qmask, tgt, local && !done && e == NONE && !(SLAB && in_role), &got);
+            if (got != NONE) {
+                e = SDF_CHK(28, got, P.c_lo, P.c_lo + P.n);   // owned: its counter moved 0 -> 1 for the requester
+                next = NONE;
+                rq = 1;
+            }
+        }
+        const bool idle_local = local && e == NONE && !(SLAB && in_role);
 #if SP_SPLIT_APPEND
-        sp_append_issue(P, shard, qmask, fin, app);
+        sp_append_issue(P, shard, qmask, fin, nloc, app);
         if (app.live) {
 #pragma unroll
             for (int q = 0; q < 7; ++q) tgt_app[q] = tgt[q];
         }
-        if (__all(done)) {
+        if (__all(done || idle_local)) {
             sp_append_finish(P, shard, tgt_app, app);
             break;
         }
 #else
-        sp_append_wave(P, shard, qmask, tgt, fin);
-        if (__all(done)) break;
+        sp_append_wave(P, shard, qmask, tgt, fin, nloc);
+        if (__all(done || idle_local)) break;
 #endif
         if (SP_IDLE_SLEEP && !__any(e != NONE)) __builtin_amdgcn_s_sleep(SP_IDLE_SLEEP);
     }

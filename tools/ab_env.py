@@ -17,7 +17,7 @@ for rep in range(6):
         digest = "ok" if got == ref else "MISMATCH"
     p = _lib.last_profile()
     if rep and (best is None or p["total_ms"] < best["total_ms"]): best = p
-print(json.dumps({k: best[k] for k in ("total_ms", "band_ms", "sweep_ms")} | {"sw": [round(x, 3) for x in best["sweep_launch_ms"]], "digest": digest if ref else "-"}))
+print(json.dumps({k: best[k] for k in ("total_ms", "band_ms", "sweep_ms", "sparse_rechecks", "sparse_claims")} | {"sw": [round(x, 3) for x in best["sweep_launch_ms"]], "digest": digest if ref else "-"}))
 ''' % (ROOT, wl)
 for rnd in range(2):
     for cfg in cfgs:
@@ -30,4 +30,4 @@ for rnd in range(2):
         if r.returncode:
             print(cfg, "FAILED", r.stderr[-800:]); sys.exit(1)
         d = json.loads(r.stdout.strip().splitlines()[-1])
-        print(f"{cfg:28s} total {d['total_ms']:7.3f} band {d['band_ms']:6.3f} sweep {d['sweep_ms']:7.3f} | tile {sum(d['sw'][:8]):6.3f} sparse {sum(d['sw'][8:]):6.3f} digest {d['digest']}", flush=True)
+        print(f"{cfg:28s} total {d['total_ms']:7.3f} band {d['band_ms']:6.3f} sweep {d['sweep_ms']:7.3f} | tile {sum(d['sw'][:8]):6.3f} sparse {sum(d['sw'][8:]):6.3f} rechecks {d['sparse_rechecks']} claims {d['sparse_claims']} digest {d['digest']}", flush=True)
