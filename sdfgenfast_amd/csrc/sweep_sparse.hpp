@@ -100,6 +100,9 @@ constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup
 #define SP_LOCAL_LANES 32   // k_sp_recheck: lanes per wave that take no ring tickets (sp_hand_local)
 #endif
 static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least one ring lane");
+#ifndef SP_JACOBI_CHUNK
+#define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
+#endif
 
 // the reference's 8 sweep directions in pass order (cpu_lib/makelevelset3.cpp:243-291)
 constexpr int SP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
@@ -575,8 +578,22 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
     const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD
     unsigned *buf = s_list[threadIdx.x >> 6];
     unsigned cnt = 0;   // wave-uniform
+#if SP_JACOBI_CHUNK
+    // Each block scans one contiguous chunk of its XCD's eighth, so blocks are dispatched in
+    // address order and the upwind plane a cell reads was just read by the blocks before it: still
+    // in the XCD's L2.  (A grid-stride loop over 2,048 blocks per XCD jumped 8 planes per step and
+    // fetched S twice from HBM: 268 MB per launch at 256^3, PMC.)
+    const unsigned long long nb = xcd ? gridDim.x / 8 : gridDim.x;
+    const unsigned long long chunk = (span + nb * blockDim.x - 1) / (nb * blockDim.x) * blockDim.x;   // = per_block of sp_reserve
+    const unsigned long long c_beg = (unsigned long long)(xcd ? blockIdx.x / 8 : blockIdx.x) * chunk;
+    const unsigned long long c_end = std::min(span, c_beg + chunk);
+    const unsigned long long first = c_beg + threadIdx.x;
+    const unsigned long long step = blockDim.x;
+#else
+    const unsigned long long c_end = span;
     const unsigned long long first = (unsigned long long)(xcd ? blockIdx.x / 8 : blockIdx.x) * blockDim.x + threadIdx.x;
     const unsigned long long step = (unsigned long long)(xcd ? gridDim.x / 8 : gridDim.x) * blockDim.x;
+#endif
     // (i, j, k) of the lane's cell: divided out once, then advanced by the stride's own
     // (si, sj, sk) with carries (two integer divisions per cell cost ~30 instructions)
     int i, j, k, si, sj, sk;
@@ -590,8 +607,8 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
         sj = (int)(rs % (unsigned)P.nj);
         sk = (int)(rs / (unsigned)P.nj);
     }
-    for (unsigned long long it = first; it - lane < span; it += step) {   // wave-uniform trip count
-        const bool valid = it < span && base + it < P.n;
+    for (unsigned long long it = first; it - lane < c_end; it += step) {   // wave-uniform trip count
+        const bool valid = it < c_end && base + it < P.n;
         const unsigned long long c = P.c_lo + base + it;
         const unsigned c32 = (unsigned)c;   // cells < 2^32 (sparse_sweep_supported)
         unsigned f = 0;
