@@ -692,6 +692,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         // repair workgroups: fewer on small grids (256^3: 64 beat 128 by 0.25 ms; 512^3: 128
         // beat 64 by 2.2 ms -- more concurrent chains there)
         ws->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
+        const char *b = getenv("SDFGEN_SPARSE_BRICK");    // 1 = the brick-owned repair (measured slower)
+        ws->sp.brick = b && atoi(b) == 1;
     }
     ws->wf.skip_seen = getenv("SDFGEN_NO_SEEN_SKIP") == nullptr;   // diagnostics
     ws->wf.clo = 0;
@@ -841,6 +843,17 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
 #ifdef SP_JACOBI_COUNT
     fprintf(stderr, "jacobi candidates %llu lane-passes %llu (slot use %.3f)\n", sp_ctl[SP_DIAG], sp_ctl[SP_DIAG + 1],
             sp_ctl[SP_DIAG + 1] ? sp_ctl[SP_DIAG] / (2.0 * sp_ctl[SP_DIAG + 1]) : 0.0);
+#endif
+#ifdef SP_ITER_PROF
+    {
+        const double nb = std::max(1.0, (double)sp_ctl[SP_DIAGX + 24]), ni = std::max(1.0, (double)sp_ctl[SP_DIAGX + 25]);
+        fprintf(stderr, "repair iterations: busy %.0f idle %.0f; cycles per busy iteration:", nb, ni);
+        for (int q = 0; q < 12; ++q) fprintf(stderr, " %.0f", sp_ctl[SP_DIAGX + q] / nb);
+        fprintf(stderr, "; per idle iteration:");
+        for (int q = 0; q < 12; ++q) fprintf(stderr, " %.0f", sp_ctl[SP_DIAGX + 12 + q] / ni);
+        fprintf(stderr, "  (ticket, tail, append wait, poll, evaluate, store, atomics, hand-off rest, append issue, "
+                        "hand-off (ballots+writes), copy+exit+sleep, join after the busy block)\n");
+    }
 #endif
     p.sparse_rechecks = sp_ctl[SP_RUNS];
     p.sparse_claims = sp_ctl[SP_ENQ];

@@ -57,7 +57,7 @@ enum { SP_ERR = 0, SP_ENQ = 1, SP_RUNS = 2, SP_DIAG = 4, SP_QUEUE = 8, SP_HEAD =
        SP_EXIT = 12, SP_OUTTAIL = 13,
        SP_JPARTS = 64, SP_JSTRIDE = 16, SP_JLIST = 16, SP_SHARD0 = SP_JLIST + SP_JPARTS * SP_JSTRIDE,
        SP_SHSTRIDE = 32, SP_MAXNQ = 16, SP_DIAGX = SP_SHARD0 + SP_MAXNQ * SP_SHSTRIDE,
-       SP_NCTL = SP_DIAGX + 8 };   // SP_DIAGX..: diagnostics accumulated over the call
+       SP_NCTL = SP_DIAGX + 32 };   // SP_DIAGX..: diagnostics accumulated over the call
 // Work-list shards (SP_NQ): shard s has its own ring (P.queue + s * P.cap), its tail+pending word
 // ctl[SP_SHARD0 + s * SP_SHSTRIDE] and its head word 16 words (128 bytes) further.  A wave appends
 // to and takes from its home shard only, so every shard is a closed system that drains on its
@@ -103,6 +103,15 @@ static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
+
+// Ring slot of work-list position t.  Positions restart at 0 every sweep and a sweep appends far
+// fewer items than a ring holds, so the 64-bit remainder (~100 instructions, x7 in an append) is
+// only a cold fallback kept out of the repair loop's hot path.
+__device__ __forceinline__ unsigned long long sp_slot(unsigned long long t, unsigned long long cap)
+{
+    if (t >= cap) t %= cap;
+    return t;
+}
 
 // the reference's 8 sweep directions in pass order (cpu_lib/makelevelset3.cpp:243-291)
 constexpr int SP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1, +1},
@@ -396,7 +405,7 @@ __device__ __forceinline__ void sp_append_wave(const SpParams &P, unsigned shard
     unsigned long long t = t0 + pre;
 #pragma unroll
     for (int q = 0; q < 7; ++q)
-        if ((qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + (t++) % P.cap, (unsigned)(tgt[q] + 1));
+        if ((qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + sp_slot(t++, P.cap), (unsigned)(tgt[q] + 1));
 }
 
 // sp_append_wave in two halves, so that the append's round trip overlaps the next iteration's
@@ -455,7 +464,7 @@ __device__ __forceinline__ void sp_append_finish(const SpParams &P, unsigned sha
     unsigned long long t = t0 + A.pre;
 #pragma unroll
     for (int q = 0; q < 7; ++q)
-        if ((A.qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + (t++) % P.cap, (unsigned)(tgt[q] + 1));
+        if ((A.qmask >> q) & 1u) sp_st32(P.queue + (size_t)shard * P.cap + sp_slot(t++, P.cap), (unsigned)(tgt[q] + 1));
 }
 
 // wave-synchronous LDS hand-over between lanes of one wave
@@ -473,12 +482,19 @@ __device__ __forceinline__ void sp_wave_sync()
 // store, the taker's tail read and slot poll): the taker evaluates it in the next iteration, like a
 // depth-first claim.  Returns the number of cells handed over (wave-uniform); *got = the taken cell.
 __device__ __forceinline__ unsigned sp_hand_local(unsigned *s_hand, unsigned *qmask, const size_t (&tgt)[7],
-                                                  bool free_lane, size_t *got)
+                                                  bool free_lane, size_t *got, unsigned long long *ipt = nullptr,
+                                                  unsigned long long *ipd = nullptr)
 {
+#ifdef SP_ITER_PROF
+#define SP_IPH(q) do { const unsigned long long t2_ = clock64(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ipd[q] += t2_ - *ipt; *ipt = t2_; } while (0)
+#else
+#define SP_IPH(q) do { } while (0)
+#endif
     const unsigned lane = threadIdx.x & 63;
     const unsigned nq = __popc(*qmask);
     const unsigned long long fm = __ballot(free_lane), b0 = __ballot(nq & 1u), b1 = __ballot(nq & 2u),
                              b2 = __ballot(nq & 4u);
+    SP_IPH(9);
     if (!fm || !(b0 | b1 | b2)) return 0u;
     const unsigned long long lt = (1ull << lane) - 1ull;
     const unsigned tot = (unsigned)(__popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2));
@@ -495,6 +511,7 @@ __device__ __forceinline__ unsigned sp_hand_local(unsigned *s_hand, unsigned *qm
             ++x;
         }
     }
+    SP_IPH(9);
     sp_wave_sync();
     const unsigned r = (unsigned)__popcll(fm & lt);
     if (free_lane && r < nloc) *got = s_hand[r];
@@ -704,10 +721,20 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
     app.old_q = 0;   // read by the unconditional wait of sp_append_finish before the first issue
     size_t tgt_app[7];   // the cells of the append in flight
 #endif
+#ifdef SP_ITER_PROF   // diagnostics: cycles per phase of an iteration, busy (>= 1 lane evaluates) or idle
+    unsigned long long ip_b[12] = {}, ip_i[12] = {}, ip_d[12], ip_t = 0, ip_nb = 0, ip_ni = 0;
+#define SP_IP(q) do { const unsigned long long t2_ = clock64(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ip_d[q] = t2_ - ip_t; ip_t = t2_; } while (0)
+#else
+#define SP_IP(q) do { } while (0)
+#endif
     for (;;) {
         unsigned qmask = 0;   // cells this lane queues this iteration (sp_append_wave below)
         size_t tgt[7];
         bool fin = false;     // this lane's work item ended this iteration
+#ifdef SP_ITER_PROF
+        for (int q = 0; q < 12; ++q) ip_d[q] = 0;
+        ip_t = clock64();
+#endif
         {
             // queue tickets for every lane that needs one: ONE atomic on the head word per wave
             const bool want = !done && e == NONE && !waiting && !(SLAB && in_role) && !local;
@@ -722,15 +749,18 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 }
             }
         }
+        SP_IP(0);
         // the shard's tail word, read once for the wave's waiting lanes
         unsigned long long qw = 0;
         if (__any(!done && e == NONE && waiting && !(SLAB && in_role))) {
             if (lane == 0) qw = sp_ld64(q_tail);
             qw = ((unsigned long long)(unsigned)__shfl((int)(qw >> 32), 0) << 32) | (unsigned)__shfl((int)qw, 0);
         }
+        SP_IP(1);
 #if SP_SPLIT_APPEND
         sp_append_finish(P, shard, tgt_app, app);   // last iteration's append (its atomic overlapped the above)
 #endif
+        SP_IP(2);
         if (SLAB && in_role && e == NONE) {
             if (!in_wait) {
                 h_in = atomicAdd(&P.ctl[SP_INHEAD], 1ull);
@@ -765,9 +795,9 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             }
         } else if (!done && e == NONE && !local) {   // a ring lane: its ticket's slot
             // the slot is read only once the tail has passed it (appended; its store may still land)
-            const unsigned v = h < (qw & 0xffffffffull) ? sp_ld32(ring + h % P.cap) : 0u;
+            const unsigned v = h < (qw & 0xffffffffull) ? sp_ld32(ring + sp_slot(h, P.cap)) : 0u;
             if (v) {
-                sp_st32(ring + h % P.cap, 0u);
+                sp_st32(ring + sp_slot(h, P.cap), 0u);
                 e = SDF_CHK(28, v - 1, P.c_lo, P.c_lo + P.n);
                 next = NONE;
                 rq = 1;
@@ -780,6 +810,12 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 done = true;
             }
         }
+        SP_IP(3);
+        // (profile: the stamps are per lane -- a lane outside the busy block keeps its last stamp --
+        // so a busy iteration is reported from its first busy lane)
+        const unsigned long long ip_bm = __ballot(e != NONE);
+        const bool ip_busy = ip_bm != 0ull;
+        (void)ip_busy;
         if (e != NONE) {
             // one evaluation of cell e, retiring `rq` requests
             const int i = (int)((unsigned)e % (unsigned)P.ni);
@@ -793,11 +829,13 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 #endif
             ++runs;
             const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
+            SP_IP(4);
             if (y != cur) {
                 sp_st64(P.X + e, y);
                 if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
             }
             if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
+            SP_IP(5);
             // retire e's requests and ask for the downstream rechecks in one round trip
             const unsigned old = atomicSub(P.req + e, rq);
             if (relabel) {
@@ -818,11 +856,22 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 rq = old - rq;   // evaluate again for the requests that arrived meanwhile
                 sp_order();
             }
+#ifdef SP_ITER_PROF
+            sp_order();   // (profile only: the request atomics' returns land inside phase 6)
+#endif
+            SP_IP(6);
         }
+#ifdef SP_ITER_PROF
+        { const unsigned long long t2_ = clock64(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); ip_d[11] += t2_ - ip_t; ip_t = t2_; }   // (join)
+#endif
         unsigned nloc = 0;
         if (SP_LOCAL_LANES) {
             size_t got = NONE;
+#ifdef SP_ITER_PROF
+            nloc = sp_hand_local(s_hand, &qmask, tgt, local && !done && e == NONE && !(SLAB && in_role), &got, &ip_t, ip_d);
+#else
             nloc = sp_hand_local(s_hand, &qmask, tgt, local && !done && e == NONE && !(SLAB && in_role), &got);
+#endif
             if (got != NONE) {
                 e = SDF_CHK(28, got, P.c_lo, P.c_lo + P.n);   // owned: its counter moved 0 -> 1 for the requester
                 next = NONE;
@@ -830,8 +879,10 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             }
         }
         const bool idle_local = local && e == NONE && !(SLAB && in_role);
+        SP_IP(7);
 #if SP_SPLIT_APPEND
         sp_append_issue(P, shard, qmask, fin, nloc, app);
+        SP_IP(8);
         if (app.live) {
 #pragma unroll
             for (int q = 0; q < 7; ++q) tgt_app[q] = tgt[q];
@@ -845,7 +896,31 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
         if (__all(done || idle_local)) break;
 #endif
         if (SP_IDLE_SLEEP && !__any(e != NONE)) __builtin_amdgcn_s_sleep(SP_IDLE_SLEEP);
+#ifdef SP_ITER_PROF
+        SP_IP(10);   // (phase 9: hand-off ballots, 11: hand-off slot writes; 7: the rest of the hand-off)
+        {
+            const int src = ip_busy ? __ffsll((long long)ip_bm) - 1 : 0;
+            for (int q = 0; q < 12; ++q) {
+                const unsigned long long v = ((unsigned long long)(unsigned)__shfl((int)(ip_d[q] >> 32), src) << 32) |
+                                             (unsigned)__shfl((int)ip_d[q], src);
+                if (ip_busy) ip_b[q] += v;
+                else ip_i[q] += v;
+            }
+        }
+        if (ip_busy) ++ip_nb;
+        else ++ip_ni;
+#endif
     }
+#ifdef SP_ITER_PROF
+    if (lane == 0) {
+        for (int q = 0; q < 12; ++q) {
+            atomicAdd(&P.ctl[SP_DIAGX + q], ip_b[q]);
+            atomicAdd(&P.ctl[SP_DIAGX + 12 + q], ip_i[q]);
+        }
+        atomicAdd(&P.ctl[SP_DIAGX + 24], ip_nb);
+        atomicAdd(&P.ctl[SP_DIAGX + 25], ip_ni);
+    }
+#endif
     if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
     if (claims) atomicAdd(&P.ctl[SP_ENQ], claims);
     if (SLAB) {
@@ -965,10 +1040,382 @@ __global__ void __launch_bounds__(256) k_sp_slab_export(SpExportParams E)
 }
 
 // ---------------------------------------------------------------------------
+// Brick-owned repair (one GPU).  The grid is cut into 8x8x8 bricks.  A repair
+// request names a cell; it sets the cell's bit in its brick's request bits and counts in the
+// brick's request counter; the request that moves the counter 0 -> 1 queues the BRICK.  A wave
+// that takes a brick owns it -- only the owner writes the brick's cells -- and repairs it in LDS:
+// the brick's cells, their pre-sweep values and the upwind halo's labels are loaded once, and the
+// requested cells and everything downstream of a relabel inside the brick are evaluated in one
+// pass over the brick's anti-diagonals in the sweep's order (a cell's upwind neighbours lie on
+// earlier diagonals, so each is final when the cell is evaluated).  A chain link inside a brick
+// then costs an LDS read instead of the cell protocol's device round trips (label loads, the
+// label store's wait, the request counters, the work list).  Relabelled cells are written back,
+// and only cells on the brick's downstream faces request cells of the next bricks.  The owner
+// retires the requests it saw; if more came meanwhile (an upwind brick changed a halo label) it
+// reloads the halo and runs again.  Exact for the same reason as the cell protocol: when the work
+// list drains, every cell satisfies x_c = f(S_c, labels(x_upwind)).
+// ---------------------------------------------------------------------------
+constexpr int SPB = 8;                     // brick edge (cells)
+constexpr int SPB_CELLS = SPB * SPB * SPB;
+constexpr int SPB_WORDS = SPB_CELLS / 32;  // request-bit words per brick
+constexpr int SPB_H = SPB + 1;             // LDS label block edge: the upwind halo layer at 0
+
+struct SpBrick {
+    unsigned *breq;                        // per brick: outstanding requests (zero between sweeps)
+    unsigned *bits;                        // per brick: SPB_WORDS request-bit words (zero between sweeps)
+    int nbi, nbj, nbk;                     // bricks per axis
+    unsigned long long nbricks;
+};
+
+// brick of global cell (i, j, k) and the cell's bit there, in the sweep's orientation (a grows
+// downstream along i whatever the sign of di; the same for b, c)
+__device__ __forceinline__ void spb_locate(const SpParams &P, const SpBrick &B, int i, int j, int k, unsigned *brick,
+                                           unsigned *bit)
+{
+    const int bi = i / SPB, bj = j / SPB, bk = k / SPB;
+    const int ei = min(SPB, P.ni - bi * SPB), ej = min(SPB, P.nj - bj * SPB), ek = min(SPB, P.nk - bk * SPB);
+    const int a = P.di > 0 ? i - bi * SPB : ei - 1 - (i - bi * SPB);
+    const int b = P.dj > 0 ? j - bj * SPB : ej - 1 - (j - bj * SPB);
+    const int c = P.dk > 0 ? k - bk * SPB : ek - 1 - (k - bk * SPB);
+    *brick = (unsigned)(bi + B.nbi * (bj + B.nbj * bk));
+    *bit = (unsigned)(a + SPB * (b + SPB * c));
+}
+
+// Request the cells tgt[q] (slots with no target: ~0): bits first, and only once they are in
+// place the counters -- an owner that counted a request finds its bit.  Bricks whose counter this
+// lane moved 0 -> 1 are this lane's to queue: slot bits in *qmask, brick ids in bq[].
+__device__ __forceinline__ void spb_request(const SpParams &P, const SpBrick &B, const size_t (&tgt)[7], unsigned *qmask,
+                                            size_t (&bq)[7])
+{
+    unsigned br[7], bt[7];
+    *qmask = 0;
+    int fq = -1;   // first slot with a target
+#pragma unroll
+    for (int q = 6; q >= 0; --q)
+        if (tgt[q] != ~(size_t)0) fq = q;
+    if (fq < 0) return;   // (a lane with no target must not touch any counter: see below)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        br[q] = 0;
+        bt[q] = 0;
+        if (tgt[q] != ~(size_t)0) {
+            const unsigned t = (unsigned)tgt[q];
+            const int i = (int)(t % (unsigned)P.ni);
+            const unsigned r = t / (unsigned)P.ni;
+            spb_locate(P, B, i, (int)(r % (unsigned)P.nj), (int)(r / (unsigned)P.nj), &br[q], &bt[q]);
+            atomicOr(&B.bits[SDF_CHK(29, (size_t)br[q] * SPB_WORDS + (bt[q] >> 5), 0, B.nbricks * SPB_WORDS)],
+                     1u << (bt[q] & 31u));
+        }
+    }
+    sp_order();   // the bits are in place before any counter moves
+    unsigned br0 = br[0];
+#pragma unroll
+    for (int q = 1; q < 7; ++q) br0 = fq == q ? br[q] : br0;
+    unsigned old[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const bool ok = tgt[q] != ~(size_t)0;
+        // branch-free (a conditional returning atomic costs a round trip each): a slot with no
+        // target adds 0 to the lane's first target brick -- never to one shared word, which every
+        // lane of every wave would hammer (a first version's 0-adds to brick 0 cost 20 ms per sweep)
+        const unsigned r = atomicAdd(&B.breq[SDF_CHK(30, ok ? br[q] : br0, 0, B.nbricks)], ok ? 1u : 0u);
+        old[q] = ok ? r : 1u;
+    }
+    unsigned qm = 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        if (old[q] != 0u) continue;
+        qm |= 1u << q;
+        bq[q] = br[q];
+    }
+    *qmask = qm;
+}
+
+// the downstream neighbours of (i, j, k) in the grid (the cells whose upwind set contains it), ~0
+// where there is none -- sp_request_collect's targets without its counters
+__device__ __forceinline__ void spb_targets(const SpParams &P, int i, int j, int k, size_t c, size_t (&tgt)[7])
+{
+    const bool ii = P.di > 0 ? i + 1 <= P.ni - 1 : i - 1 >= 0;
+    const bool jj = P.dj > 0 ? j + 1 <= P.nj - 1 : j - 1 >= 0;
+    const bool kk = P.dk > 0 ? k + 1 <= P.nk - 1 : k - 1 >= 0;
+    const long long si = P.di, sj = (long long)P.dj * P.ni, sk = (long long)P.dk * P.ni * P.nj;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        const int m = q + 1;
+        const bool ui = m & 1, uj = m & 2, uk = m & 4;
+        const bool ok = !((ui && !ii) || (uj && !jj) || (uk && !kk));
+        tgt[q] = ok ? (size_t)((long long)c + (ui ? si : 0) + (uj ? sj : 0) + (uk ? sk : 0)) : ~(size_t)0;
+    }
+}
+
+// Jacobi list pass, brick mode: the listed cells as in k_sp_jlist; a relabel requests its 7
+// downstream cells from their bricks.
+__global__ void __launch_bounds__(256) k_sp_jlist_brick(SpParams P, SpBrick B)
+{
+    const unsigned part = blockIdx.x % SP_JPARTS;
+    const unsigned long long cnt0 = P.ctl[SP_JLIST + part * SP_JSTRIDE];
+    const unsigned long long cnt = cnt0 < P.jcap ? cnt0 : P.jcap;
+    const unsigned *list = P.jlist + (size_t)part * P.jcap;
+    const unsigned lane = threadIdx.x & 63;
+    for (unsigned long long x = (unsigned long long)(blockIdx.x / SP_JPARTS) * blockDim.x + threadIdx.x; x - lane < cnt;
+         x += (unsigned long long)(gridDim.x / SP_JPARTS) * blockDim.x) {
+        unsigned qmask = 0;
+        size_t tgt[7], bq[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) tgt[q] = ~(size_t)0;
+        if (x < cnt) {
+            const unsigned c32 = list[x];
+            const int i = (int)(c32 % (unsigned)P.ni);
+            const unsigned r = c32 / (unsigned)P.ni;
+            const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
+            const unsigned long long s = P.S[SDF_CHK(20, c32, P.c_lo, P.c_lo + P.n)];
+            const unsigned long long y = sp_eval<false>(P, P.S, i, j, k, c32, s);
+            P.X[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = y;
+            if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) spb_targets(P, i, j, k, c32, tgt);
+        }
+        // (the brick kernel reads the labels after this launch: no wait needed before the requests)
+        spb_request(P, B, tgt, &qmask, bq);
+        sp_append_wave(P, (unsigned)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (P.nq - 1u)), qmask, bq, false);
+    }
+}
+
+// The brick repair: one wave per workgroup, one brick at a time.  Lane (b, c) = (lane % 8,
+// lane / 8) owns the brick's row (b, c): its 8 cells along a, their loads and write-backs; on
+// anti-diagonal d it evaluates cell (d - b - c, b, c), so no lane needs a table to find its cell.
+__global__ void __launch_bounds__(64) k_sp_brick(SpParams P, SpBrick B)
+{
+    __shared__ unsigned long long s_x[SPB_CELLS];      // the brick's cells (current), oriented index
+    __shared__ unsigned long long s_s[SPB_CELLS];      // ... before the sweep
+    __shared__ uint32_t s_w[SPB_H * SPB_H * SPB_H];    // low words with the upwind halo layer at 0
+    __shared__ uint32_t s_f[SPB_WORDS];                // cells to evaluate
+    const unsigned lane = threadIdx.x & 63;
+    const int rb = (int)(lane % SPB), rc = (int)(lane / SPB);   // this lane's row
+    const unsigned shard = blockIdx.x & (P.nq - 1u);
+    unsigned long long *const q_tail = &P.ctl[SP_SHARD0 + shard * SP_SHSTRIDE];
+    unsigned long long *const q_head = q_tail + 16;
+    unsigned *const ring = P.queue + (size_t)shard * P.cap;
+    unsigned long long runs = 0, h = 0;
+    bool ticket = false;
+    unsigned spins = 0;
+#ifdef SP_ITER_PROF   // diagnostics: cycles per phase of a brick activation, activations, rounds
+    unsigned long long bp[8] = {}, bp_t = 0, bp_act = 0, bp_rounds = 0;
+#define SPB_P(q) do { const unsigned long long t2_ = clock64(); asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); bp[q] += t2_ - bp_t; bp_t = t2_; } while (0)
+#else
+#define SPB_P(q) do { } while (0)
+#endif
+    for (;;) {
+        // ---- take a brick: one ticket per wave; the slot is read once the tail has passed it ----
+        unsigned long long qw = 0, base = 0;
+        unsigned v = 0;
+        if (lane == 0) {
+            if (!ticket) base = atomicAdd(q_head, 1ull);
+            qw = sp_ld64(q_tail);
+        }
+        if (!ticket) {
+            h = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), 0) << 32) | (unsigned)__shfl((int)base, 0);
+            ticket = true;
+        }
+        qw = ((unsigned long long)(unsigned)__shfl((int)(qw >> 32), 0) << 32) | (unsigned)__shfl((int)qw, 0);
+        if (lane == 0 && h < (qw & 0xffffffffull)) v = sp_ld32(ring + sp_slot(h, P.cap));
+        v = (unsigned)__shfl((int)v, 0);
+        if (!v) {
+            if ((qw >> 32) == 0ull) break;   // nothing queued or running in this shard: no slot can fill
+            if (++spins > SP_WATCHDOG) {
+                if (lane == 0) atomicOr(&P.ctl[SP_ERR], 1ull);
+                break;
+            }
+            // back off: most waves are idle most of the time, and their polls of the shard words
+            // slowed every other device access of the launch (a 4 us round trip at a 2 us poll)
+            if (spins < 4) __builtin_amdgcn_s_sleep(1);
+            else if (spins < 32) __builtin_amdgcn_s_sleep(4);
+            else __builtin_amdgcn_s_sleep(16);
+            continue;
+        }
+        if (lane == 0) sp_st32(ring + sp_slot(h, P.cap), 0u);
+        ticket = false;
+        spins = 0;
+#ifdef SP_ITER_PROF
+        bp_t = clock64();
+        ++bp_act;
+#endif
+        const unsigned brick = SDF_CHK(31, v - 1, 0, B.nbricks);
+        const int bi = (int)(brick % (unsigned)B.nbi), bt = (int)(brick / (unsigned)B.nbi);
+        const int bj = bt % B.nbj, bk = bt / B.nbj;
+        const int i0 = bi * SPB, j0 = bj * SPB, k0 = bk * SPB;
+        const int ea = min(SPB, P.ni - i0), eb = min(SPB, P.nj - j0), ec = min(SPB, P.nk - k0);
+        // oriented local (a, b, c) -> global: a grows in the sweep's i direction (-1: the upwind halo)
+        const int ia0 = P.di > 0 ? i0 : i0 + ea - 1, sa = P.di;
+        const int jb0 = P.dj > 0 ? j0 : j0 + eb - 1, sb = P.dj;
+        const int kc0 = P.dk > 0 ? k0 : k0 + ec - 1, sc = P.dk;
+        const long long rowstride = (long long)P.ni;
+        const long long planestride = (long long)P.ni * P.nj;
+        auto gidx = [&](int a, int b, int c) -> long long {
+            return (long long)(ia0 + sa * a) + rowstride * (jb0 + sb * b) + planestride * (kc0 + sc * c);
+        };
+        auto ingrid = [&](int a, int b, int c) {
+            const int i = ia0 + sa * a, j = jb0 + sb * b, k = kc0 + sc * c;
+            return i >= 0 && i < P.ni && j >= 0 && j < P.nj && k >= 0 && k < P.nk;
+        };
+        const bool row_in = rb < eb && rc < ec;
+        bool first = true;
+        unsigned chg = 0, rel = 0;   // this lane's row: cells changed / relabelled (bit a)
+        for (;;) {
+            // requests so far, then their bits (requesters set the bit before counting)
+            unsigned r = 0;
+            if (lane == 0) r = sp_ld32(&B.breq[brick]);
+            if (lane < SPB_WORDS) s_f[lane] = atomicExch(&B.bits[(size_t)brick * SPB_WORDS + lane], 0u);
+            r = (unsigned)__shfl((int)r, 0);
+            sp_order();   // the cells and halo are read after the requests were observed
+            SPB_P(0);
+#ifdef SP_ITER_PROF
+            ++bp_rounds;
+#endif
+            // loads, all issued before the first is used: the row's cells (first round only -- the
+            // owner is their only writer) and the upwind halo: the row's a = -1 cell, and 3 more
+            // positions per lane for the b = -1 and c = -1 faces (9 x 9 + 9 x 8 = 153)
+            unsigned long long xr[SPB], sr[SPB];
+            uint32_t hr = 0, hf[3] = {0u, 0u, 0u};
+            if (first && row_in) {
+#pragma unroll
+                for (int a = 0; a < SPB; ++a) {
+                    if (a < ea) {
+                        const size_t g = SDF_CHK(32, gidx(a, rb, rc), 0, P.n);
+                        xr[a] = sp_ld64(P.X + g);
+                        sr[a] = P.S[g];
+                    }
+                }
+            }
+            if (row_in && ingrid(-1, rb, rc))
+                hr = sp_ld32(reinterpret_cast<const uint32_t *>(P.X + SDF_CHK(32, gidx(-1, rb, rc), 0, P.n)));
+            int fa[3], fb[3], fc[3];
+#pragma unroll
+            for (int u = 0; u < 3; ++u) {
+                const int t = (int)lane + 64 * u;   // 0..152: (a, -1, c) for c = -1..7, then (a, b, -1) for b = 0..7
+                fa[u] = t % SPB_H - 1;
+                fb[u] = t < 81 ? -1 : (t - 81) / SPB_H;
+                fc[u] = t < 81 ? t / SPB_H - 1 : -1;
+                if (t < 153 && fa[u] < ea && fb[u] < eb && fc[u] < ec && ingrid(fa[u], fb[u], fc[u]))
+                    hf[u] = sp_ld32(reinterpret_cast<const uint32_t *>(P.X + SDF_CHK(32, gidx(fa[u], fb[u], fc[u]), 0, P.n)));
+            }
+            if (first && row_in) {
+#pragma unroll
+                for (int a = 0; a < SPB; ++a) {
+                    if (a < ea) {
+                        const int o = a + SPB * (rb + SPB * rc);
+                        s_x[o] = xr[a];
+                        s_s[o] = sr[a];
+                        s_w[(a + 1) + SPB_H * ((rb + 1) + SPB_H * (rc + 1))] = (uint32_t)xr[a];
+                    }
+                }
+            }
+            if (row_in) s_w[0 + SPB_H * ((rb + 1) + SPB_H * (rc + 1))] = hr;
+#pragma unroll
+            for (int u = 0; u < 3; ++u)
+                if ((int)lane + 64 * u < 153) s_w[(fa[u] + 1) + SPB_H * ((fb[u] + 1) + SPB_H * (fc[u] + 1))] = hf[u];
+            first = false;
+            sp_wave_sync();
+            SPB_P(1);
+            // one pass over the anti-diagonals in the sweep's order
+            const int dmax = ea + eb + ec - 3;
+            for (int d = 0; d <= dmax; ++d) {
+                const int a = d - rb - rc;
+                const int o = a + SPB * (rb + SPB * rc);
+                const bool act = row_in && a >= 0 && a < ea && ((s_f[o >> 5] >> (o & 31)) & 1u);
+                if (!__any(act)) continue;
+                if (act) {
+                    const int i = ia0 + sa * a, j = jb0 + sb * rb, k = kc0 + sc * rc;
+                    if (sp_in(P, i, j, k)) {
+                        uint32_t w[7];
+#pragma unroll
+                        for (int q = 0; q < 7; ++q) {
+                            const int m = q + 1;
+                            w[q] = s_w[(a + 1 - (m & 1)) + SPB_H * ((rb + 1 - ((m >> 1) & 1)) + SPB_H * (rc + 1 - ((m >> 2) & 1)))];
+                        }
+                        const unsigned long long cur = s_x[o];
+                        const unsigned long long y = sp_eval_w<true>(P, i, j, k, s_s[o], w);
+                        ++runs;
+                        if (y != cur) {
+                            s_x[o] = y;
+                            s_w[(a + 1) + SPB_H * ((rb + 1) + SPB_H * (rc + 1))] = (uint32_t)y;
+                            chg |= 1u << a;
+                            if (lbl_of((uint32_t)y) != lbl_of((uint32_t)cur)) {
+                                // downstream cells inside the brick: later diagonals of this pass
+#pragma unroll
+                                for (int m = 1; m < 8; ++m) {
+                                    const int a2 = a + (m & 1), b2 = rb + ((m >> 1) & 1), c2 = rc + ((m >> 2) & 1);
+                                    if (a2 < ea && b2 < eb && c2 < ec) {
+                                        const int o2 = a2 + SPB * (b2 + SPB * c2);
+                                        atomicOr(&s_f[o2 >> 5], 1u << (o2 & 31));
+                                    }
+                                }
+                                if (a == ea - 1 || rb == eb - 1 || rc == ec - 1) rel |= 1u << a;
+                            }
+                        }
+                    }
+                }
+                sp_wave_sync();
+            }
+            SPB_P(2);
+            // write back what changed, then (once it is visible) request the next bricks' cells
+#pragma unroll
+            for (int a = 0; a < SPB; ++a)
+                if ((chg >> a) & 1u)
+                    sp_st64(P.X + SDF_CHK(33, gidx(a, rb, rc), 0, P.n), s_x[a + SPB * (rb + SPB * rc)]);
+            chg = 0;
+            sp_order();
+            SPB_P(3);
+            while (__any(rel != 0u)) {
+                size_t tgt[7], bq[7];
+                unsigned qmask = 0;
+#pragma unroll
+                for (int q = 0; q < 7; ++q) tgt[q] = ~(size_t)0;
+                if (rel) {
+                    const int a = __builtin_ctz(rel);
+                    rel &= rel - 1u;
+                    size_t all[7];
+                    spb_targets(P, ia0 + sa * a, jb0 + sb * rb, kc0 + sc * rc, (size_t)gidx(a, rb, rc), all);
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {   // only the targets outside this brick
+                        const int m = q + 1;
+                        const bool out = a + (m & 1) >= ea || rb + ((m >> 1) & 1) >= eb || rc + ((m >> 2) & 1) >= ec;
+                        tgt[q] = out ? all[q] : ~(size_t)0;
+                    }
+                }
+                spb_request(P, B, tgt, &qmask, bq);
+                sp_append_wave(P, shard, qmask, bq, false);
+            }
+            SPB_P(4);
+            // retire the requests this round saw; more arrived meanwhile: run again
+            unsigned old = 0;
+            if (lane == 0) old = atomicSub(&B.breq[brick], r);
+            old = (unsigned)__shfl((int)old, 0);
+            sp_wave_sync();
+            if (old == r) break;
+        }
+        size_t none[7];
+#pragma unroll
+        for (int q = 0; q < 7; ++q) none[q] = 0;
+        sp_append_wave(P, shard, 0u, none, lane == 0);   // the brick's work item ends
+        SPB_P(5);
+    }
+    if (runs) atomicAdd(&P.ctl[SP_RUNS], runs);
+#ifdef SP_ITER_PROF
+    if (lane == 0) {
+        for (int q = 0; q < 6; ++q) atomicAdd(&P.ctl[SP_DIAGX + q], bp[q]);
+        atomicAdd(&P.ctl[SP_DIAGX + 24], bp_act);
+        atomicAdd(&P.ctl[SP_DIAGX + 25], bp_rounds);
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
 struct SparseSweepWorkspace {
     int workers = SP_WORKERS_DEFAULT;            // repair-kernel workgroups (diagnostics may lower it)
+    bool brick = false;                          // one GPU: brick-owned repair (k_sp_brick) instead of per cell
+    unsigned *breq = nullptr, *bbits = nullptr;  // brick request counters and bits (zero between sweeps)
+    size_t cap_breq = 0, cap_bbits = 0;
     unsigned long long ntri = ~0ull;             // soup size for bounds-checked builds
     unsigned long long *alt = nullptr;   // the second state buffer
     unsigned *req = nullptr, *queue = nullptr, *jlist = nullptr;
@@ -1093,13 +1540,31 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, 0, n, P, blocks)) return rc;
     P.S = *cell;
     P.X = W.alt;
-    hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
-    if (hipGetLastError() != hipSuccess) return -4;
-    const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
-    hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
-    if (hipGetLastError() != hipSuccess) return -4;
-    hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
-    if (hipGetLastError() != hipSuccess) return -4;
+    if (W.brick) {
+        SpBrick B;
+        B.nbi = (ni + SPB - 1) / SPB;
+        B.nbj = (nj + SPB - 1) / SPB;
+        B.nbk = (nk + SPB - 1) / SPB;
+        B.nbricks = (unsigned long long)B.nbi * B.nbj * B.nbk;
+        if (sp_grow(&W.breq, &W.cap_breq, B.nbricks, true, st)) return -5;
+        if (sp_grow(&W.bbits, &W.cap_bbits, B.nbricks * SPB_WORDS, true, st)) return -5;
+        B.breq = W.breq;
+        B.bits = W.bbits;
+        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+        hipLaunchKernelGGL(k_sp_jlist_brick, dim3(32 * SP_JPARTS), dim3(256), 0, st, P, B);
+        if (hipGetLastError() != hipSuccess) return -4;
+        hipLaunchKernelGGL(k_sp_brick, dim3(nw), dim3(64), 0, st, P, B);
+        if (hipGetLastError() != hipSuccess) return -4;
+    } else {
+        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+        const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
+        hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+        hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+    }
     // swap the state buffers (both hold n cells)
     unsigned long long *t = *cell;
     const size_t tc = *cap_cell;
@@ -1199,6 +1664,8 @@ inline void sparse_sweep_release(SparseSweepWorkspace &W)
     (void)hipFree(W.queue);
     (void)hipFree(W.jlist);
     (void)hipFree(W.ctl);
+    (void)hipFree(W.breq);
+    (void)hipFree(W.bbits);
     W = SparseSweepWorkspace();
 }
 

@@ -138,6 +138,19 @@ def test_gpu_full_size_matches_reference_hash(name):
     assert _hash_i_fastest(got) == rec["sha256_phi"]
 
 
+def test_gpu_brick_repair_full_size_matches_reference_hash(monkeypatch):
+    """The brick-owned repair (SDFGEN_SPARSE_BRICK=1) at C3 size against the reference digest."""
+    db = _hashes()
+    name = "c3_sphere1m_256"
+    if name not in db:
+        pytest.skip(f"{name}: no reference digest recorded")
+    monkeypatch.setenv("SDFGEN_SPARSE_BRICK", "1")
+    v, t, o, dx, dims = meshgen.workload(name)
+    got = _lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_ARRAY3)
+    assert _lib.last_profile()["sparse_sweeps"] == 8
+    assert _hash_i_fastest(got) == db[name]["sha256_phi"]
+
+
 # ---------------------------------------------------------------- contracts
 def test_gpu_bad_index_raises():
     v = np.eye(3, dtype=np.float32)
@@ -190,14 +203,17 @@ def test_gpu_device_entry_with_device_buffers():
 # ---------------------------------------------------------------- both sweep implementations
 # plane: one launch per hyperplane; tile: the column wavefront for all 16 sweeps;
 # hybrid (default): wavefront for the first pass, Jacobi + repair for the second;
-# sparse: Jacobi + repair for all 16 (stresses the repair protocol: most labels change).
+# sparse: Jacobi + repair for all 16 (stresses the repair protocol: most labels change);
+# *-brick: the same with the brick-owned repair (sweep_sparse.hpp k_sp_brick, not the default).
 SWEEP_MODES = {"plane": ({"SDFGEN_SWEEP": "plane"}, 0), "tile": ({"SDFGEN_SPARSE_FROM": "16"}, 1),
-               "hybrid": ({}, 2), "sparse": ({"SDFGEN_SPARSE_FROM": "0"}, 2)}
+               "hybrid": ({}, 2), "sparse": ({"SDFGEN_SPARSE_FROM": "0"}, 2),
+               "hybrid-brick": ({"SDFGEN_SPARSE_BRICK": "1"}, 2),
+               "sparse-brick": ({"SDFGEN_SPARSE_FROM": "0", "SDFGEN_SPARSE_BRICK": "1"}, 2)}
 
 
 @pytest.fixture(params=list(SWEEP_MODES))
 def sweep_impl(request, monkeypatch):
-    for k in ("SDFGEN_SWEEP", "SDFGEN_SPARSE_FROM"):
+    for k in ("SDFGEN_SWEEP", "SDFGEN_SPARSE_FROM", "SDFGEN_SPARSE_BRICK"):
         monkeypatch.delenv(k, raising=False)
     env, _ = SWEEP_MODES[request.param]
     for k, val in env.items():
@@ -222,6 +238,6 @@ def test_gpu_sweep_impls_agree_with_oracle(sweep_impl, nu, nv, dims):
     got = _lib.make_level_set3(v, t, o, dx, *dims, 1)
     prof = _lib.last_profile()
     assert prof["sweep_impl"] == SWEEP_MODES[sweep_impl][1]
-    if sweep_impl == "sparse":
+    if sweep_impl.startswith("sparse"):
         assert prof["sparse_sweeps"] == 16 and prof["sparse_rechecks"] > 0
     assert bits_equal(got, want), diff_report(got, want, dx)
