@@ -694,6 +694,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
         const char *b = getenv("SDFGEN_SPARSE_BRICK");    // 1 = the brick-owned repair (measured slower)
         ws->sp.brick = b && atoi(b) == 1;
+        const char *ip = getenv("SDFGEN_SPARSE_INPLACE");  // diagnostics: 0 = two buffers, swapped per sweep
+        ws->sp.inplace = !(ip && atoi(ip) == 0);
     }
     ws->wf.skip_seen = getenv("SDFGEN_NO_SEEN_SKIP") == nullptr;   // diagnostics
     ws->wf.clo = 0;

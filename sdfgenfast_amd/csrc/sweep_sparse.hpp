@@ -121,6 +121,9 @@ struct SpParams {
     const float4 *soup;                // 3 float4 per triangle
     const unsigned long long *S;       // (phi bits << 32) | label before the sweep, i-fastest
     unsigned long long *X;             // result of the sweep
+    unsigned long long *sv;            // in place (S == X; one GPU): the pre-sweep value of every cell
+                                       // that changed in this sweep, stored before its first change
+                                       // (its stamp says it changed); null: S and X are two buffers
     unsigned *req;                     // per-cell recheck requests (zero between sweeps)
     unsigned *queue;                   // ring of cell+1 (0 = empty)
     unsigned *jlist;                   // Jacobi list: SP_JPARTS parts of jcap cells
@@ -559,7 +562,12 @@ __device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32, 
     const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
     const unsigned long long s = P.S[SDF_CHK(20, c32, P.c_lo, P.c_lo + P.n)];
     const unsigned long long y = sp_eval<false, SLAB>(P, P.S, i, j, k, c32, s);
-    P.X[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = y;
+    if (!P.sv) {
+        P.X[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = y;
+    } else if (y != s) {   // in place: keep the pre-sweep value, then change the cell
+        P.sv[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = s;
+        P.X[c32] = y;
+    }
     if (lbl_of((uint32_t)y) != lbl_of((uint32_t)s)) {
         if (SLAB) sp_push(P, i, j, k, c32, (uint32_t)y);
         sp_request_collect(P, i, j, k, c32, false, qmask, tgt);
@@ -633,7 +641,7 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
             const unsigned long long s = P.S[c];
             int lab[7];
             if (sp_in(P, i, j, k)) f = sp_mask<false, SLAB>(P, P.S, i, j, k, c, s, lab);
-            if (!f) P.X[c] = s;
+            if (!f && !P.sv) P.X[c] = s;   // (in place the cell already holds it)
         }
         const unsigned long long want = __ballot(f != 0u);
         if (f) buf[cnt + __builtin_popcountll(want & ((1ull << lane) - 1ull))] = c32;
@@ -822,17 +830,22 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             const unsigned r0 = (unsigned)e / (unsigned)P.ni;
             const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
             const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, e, P.c_lo, P.c_lo + P.n));
+            // f's own input is the cell's pre-sweep value: in place, a cell stamped with this sweep
+            // has changed already and keeps it in sv
+            const bool moved = P.sv && lc_of((uint32_t)cur) == P.sweep + 1;
 #ifdef SP_NOEVAL_RECHECK   // diagnostics: the work list's own cost (no evaluation, no relabel)
             const unsigned long long y = cur;
 #else
-            const unsigned long long y = sp_eval<true, SLAB>(P, P.X, i, j, k, e, P.S[e]);
+            const unsigned long long own = !P.sv ? P.S[e] : moved ? sp_ld64(P.sv + e) : cur;
+            const unsigned long long y = sp_eval<true, SLAB>(P, P.X, i, j, k, e, own);
 #endif
             ++runs;
             const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);
             SP_IP(4);
             if (y != cur) {
+                if (P.sv && !moved) sp_st64(P.sv + e, cur);   // its first change in this sweep
                 sp_st64(P.X + e, y);
-                if (relabel) sp_order();   // the new label is visible before anyone is asked to read it
+                if (relabel || P.sv) sp_order();   // the new label (and sv) are visible before anyone reads them
             }
             if (SLAB && relabel) sp_push(P, i, j, k, e, (uint32_t)y);
             SP_IP(5);
@@ -1414,6 +1427,7 @@ __global__ void __launch_bounds__(64) k_sp_brick(SpParams P, SpBrick B)
 struct SparseSweepWorkspace {
     int workers = SP_WORKERS_DEFAULT;            // repair-kernel workgroups (diagnostics may lower it)
     bool brick = false;                          // one GPU: brick-owned repair (k_sp_brick) instead of per cell
+    bool inplace = true;                         // one GPU, per-cell repair: sweep in place (SpParams::sv)
     unsigned *breq = nullptr, *bbits = nullptr;  // brick request counters and bits (zero between sweeps)
     size_t cap_breq = 0, cap_bbits = 0;
     unsigned long long ntri = ~0ull;             // soup size for bounds-checked builds
@@ -1538,9 +1552,9 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     SpParams P;
     unsigned long long blocks = 0;
     if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, 0, n, P, blocks)) return rc;
-    P.S = *cell;
-    P.X = W.alt;
     if (W.brick) {
+        P.S = *cell;
+        P.X = W.alt;
         SpBrick B;
         B.nbi = (ni + SPB - 1) / SPB;
         B.nbj = (nj + SPB - 1) / SPB;
@@ -1556,7 +1570,21 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         if (hipGetLastError() != hipSuccess) return -4;
         hipLaunchKernelGGL(k_sp_brick, dim3(nw), dim3(64), 0, st, P, B);
         if (hipGetLastError() != hipSuccess) return -4;
+    } else if (W.inplace) {
+        // in place: the cells that keep their value (~99.9 %) are neither copied nor swapped
+        P.S = *cell;
+        P.X = *cell;
+        P.sv = W.alt;
+        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+        hipLaunchKernelGGL(k_sp_jlist<false>, dim3(32 * SP_JPARTS), dim3(256), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+        hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
+        if (hipGetLastError() != hipSuccess) return -4;
+        return 0;
     } else {
+        P.S = *cell;
+        P.X = W.alt;
         hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
         const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
