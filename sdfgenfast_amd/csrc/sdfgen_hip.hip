@@ -1204,10 +1204,13 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     if (nsw_env && atoi(nsw_env) <= 8) {
         for (int s = 8; s < 16; ++s) HIPCHK(hipEventRecord(ev[3 + s], st));
     } else if (do_sweep && sparse) {
-        // second pass as Jacobi + repair per slab: the state alternates between cell and alt
+        // second pass as Jacobi + repair per slab, in place (alt keeps the changed cells' pre-sweep
+        // values) unless SDFGEN_SPARSE_INPLACE=0: then the state alternates between cell and alt
         {
             const char *e = getenv("SDFGEN_SPARSE_WORKERS");
             S->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
+            const char *ip = getenv("SDFGEN_SPARSE_INPLACE");
+            S->sp.inplace = !(ip && atoi(ip) == 0);
         }
         // our boundary planes into the neighbours' parity-0 halo planes, then DONE
         SpExportParams E;
@@ -1238,7 +1241,8 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
             SpSlabSweep L;
             memset(&L, 0, sizeof(L));
             L.S = cur;
-            L.X = other;
+            L.X = S->sp.inplace ? cur : other;   // in place: `other` keeps the changed cells' pre-sweep values
+            L.sv = S->sp.inplace ? other : nullptr;
             L.k_lo = S->k_begin;
             L.k_hi = S->k_end;
             for (int side = 0; side < 2; ++side) {
@@ -1262,7 +1266,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
                 return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse sweep setup failed");
             S->launches += 3;
             ++S->sparse_sweeps;
-            std::swap(cur, other);
+            if (!S->sp.inplace) std::swap(cur, other);
         }
         for (int m = n_sparse; m < 8; ++m) HIPCHK(hipEventRecord(ev[11 + m], st));
     } else {

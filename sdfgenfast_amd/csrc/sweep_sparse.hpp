@@ -1607,7 +1607,8 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
 // lower neighbour (planes below k_lo), 1 = the upper one.
 struct SpSlabSweep {
     const unsigned long long *S;       // pre-sweep state, global cell index (own planes only)
-    unsigned long long *X;             // result, global cell index
+    unsigned long long *X;             // result, global cell index (== S: in place, with sv)
+    unsigned long long *sv;            // in place: pre-sweep values of changed cells (SpParams::sv); else null
     int k_lo, k_hi;
     const uint32_t *hS[2];             // our pre-sweep halo planes
     uint32_t *hX[2];                   // our live halo planes
@@ -1654,6 +1655,7 @@ inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const floa
                        dim3(256), 0, st, H);
     P.S = L.S;
     P.X = L.X;
+    P.sv = L.sv;
     P.k_lo = L.k_lo;
     P.k_hi = L.k_hi;
     const int up = P.dk > 0 ? 0 : 1, down = 1 - up;
