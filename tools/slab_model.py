@@ -26,15 +26,15 @@ import json
 
 # ---- measured inputs (one MI355X, round 3) ----
 INPUTS = {
-    "c3_sphere1m_256": {   # bench r03c: 18.52 ms total; tile launch 13.87 ms; 8 sparse sweeps 3.55 ms
-        "dims": (256, 256, 256), "t_local": 0.8650, "t_first": 13.866, "t_second": 3.5525,
-        "t_repair_per_sweep": 0.280,   # k_sp_recheck avg at C3 (rocprof r03b), the chain part of a sweep
-        "t_first_work": 5.6,           # tile work at full throughput: C4's 45.0 ms x 1/8 of the cells
+    "c3_sphere1m_256": {   # bench r03h: 17.82 ms total; tile launch 13.85 ms; 8 sparse sweeps 3.05 ms
+        "dims": (256, 256, 256), "t_local": 0.8492, "t_first": 13.846, "t_second": 3.0499,
+        "t_repair_per_sweep": 0.244,   # k_sp_recheck per sweep at C3 (r03g kernel trace, mean of 8)
+        "t_first_work": 5.6,           # tile work at full throughput: C4's first pass x 1/8 of the cells
     },
-    "c4_sphere1m_512": {   # bench r03c zslab_c4 side object: 64.74 ms; tile 45.0 ms; sparse 17.5 ms
-        "dims": (512, 512, 512), "t_local": 1.9414, "t_first": 45.001, "t_second": 17.5045,
+    "c4_sphere1m_512": {   # bench r03h zslab_c4 side object: 59.79 ms; tile 44.86 ms; sparse 12.78 ms
+        "dims": (512, 512, 512), "t_local": 1.9689, "t_first": 44.862, "t_second": 12.7841,
         "t_repair_per_sweep": 0.62,    # repair_ms per sweep, 2-slab rehearsal (r03c_n2 zslab_c4), median
-        "t_first_work": 45.0,          # throughput-bound at one GPU: the launch itself
+        "t_first_work": 44.862,        # throughput-bound at one GPU: the launch itself
     },
 }
 S_ISO_US = 1.559     # isolated tile step (bench latency probe, 1024x9x9 grid)
