@@ -204,16 +204,18 @@ def test_gpu_device_entry_with_device_buffers():
 # plane: one launch per hyperplane; tile: the column wavefront for all 16 sweeps;
 # hybrid (default): wavefront for the first pass, Jacobi + repair for the second;
 # sparse: Jacobi + repair for all 16 (stresses the repair protocol: most labels change);
-# *-brick: the same with the brick-owned repair (sweep_sparse.hpp k_sp_brick, not the default).
+# *-brick: the same with the brick-owned repair (sweep_sparse.hpp k_sp_brick, not the default);
+# *-2buf: the repair on two swapped buffers instead of in place (SpParams::sv, the default).
 SWEEP_MODES = {"plane": ({"SDFGEN_SWEEP": "plane"}, 0), "tile": ({"SDFGEN_SPARSE_FROM": "16"}, 1),
                "hybrid": ({}, 2), "sparse": ({"SDFGEN_SPARSE_FROM": "0"}, 2),
+               "sparse-2buf": ({"SDFGEN_SPARSE_FROM": "0", "SDFGEN_SPARSE_INPLACE": "0"}, 2),
                "hybrid-brick": ({"SDFGEN_SPARSE_BRICK": "1"}, 2),
                "sparse-brick": ({"SDFGEN_SPARSE_FROM": "0", "SDFGEN_SPARSE_BRICK": "1"}, 2)}
 
 
 @pytest.fixture(params=list(SWEEP_MODES))
 def sweep_impl(request, monkeypatch):
-    for k in ("SDFGEN_SWEEP", "SDFGEN_SPARSE_FROM", "SDFGEN_SPARSE_BRICK"):
+    for k in ("SDFGEN_SWEEP", "SDFGEN_SPARSE_FROM", "SDFGEN_SPARSE_BRICK", "SDFGEN_SPARSE_INPLACE"):
         monkeypatch.delenv(k, raising=False)
     env, _ = SWEEP_MODES[request.param]
     for k, val in env.items():
