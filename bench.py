@@ -280,11 +280,15 @@ def _build_id():
     return _lib.build_id()
 
 
-def roofline(r, step_us, workload):
+def roofline(r, step_us, workload, whole_grid=True):
+    """whole_grid=False (a Z-slab rank): the PMC summary holds the ONE-GPU launch over the whole
+    grid, not this slab's launch, so no traffic is reported for it."""
     achieved = r["bytes_per_launch"] / (r["launch_ms"] * 1e-3) / 1e9 if r["launch_ms"] > 0 else 0.0
     traffic, traffic_src = None, None
     tp = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if os.path.exists(tp):
+    if not whole_grid:
+        traffic_src = "n/a: profiles/pmc_summary.json is the one-GPU whole-grid launch, not a slab's"
+    elif os.path.exists(tp):
         rec = json.load(open(tp))
         k = rec.get("kernels", {}).get("k_sweep_tile")
         if rec.get("workload") == workload and k:
@@ -458,7 +462,7 @@ def main():
             "config": {"workload": args.workload, "grid": [ni, nj, nk], "triangles": r["triangles"],
                        "exact_band": 1, "parallelism": parallelism, "inputs": "HBM-resident",
                        "ranks_per_gpu": (world + ndev - 1) // ndev},
-            "roofline": roofline(r, step_us, args.workload),
+            "roofline": roofline(r, step_us, args.workload, whole_grid=(world == 1 or parallelism.startswith("replica"))),
             "valu": valu(r, args.workload) if world == 1 else None,
             "phases_ms": r["phases"],
             "sweep_impl": r["sweep_impl"],
