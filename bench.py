@@ -82,7 +82,9 @@ def cpu_baseline(workload: str):
         return {"value": round(n / el / 1e6, 4), "unit": "Mvoxels/s", "cores": th, "kind": "reference",
                 "sample": f"reference cpu_lib make_level_set3 (oracle/_ref, built from /root/reference), "
                           f"num_threads={th}, the full {workload} workload ({n} voxels, {t.shape[0]} triangles), "
-                          f"{el:.2f} s; 1 thread: tests/golden/hashes.json ref_seconds_1thread. Timing only: with "
+                          f"{el:.2f} s; 1 thread on an MI355X box host (EPYC 9575F): 42.3 s, 0.397 Mvoxels/s "
+                          f"(profiles/r03_ref_1thread_box.log; 89.3 s in the build container: tests/golden/hashes.json "
+                          f"ref_seconds_1thread). Timing only: with "
                           f"{th} threads the reference's k-split sweep races (SURVEY K1), so its output is not "
                           f"parity-valid (the parity target is its 1-thread result)"}
     log("bench: oracle/_ref (the reference build) is absent -- timing the native CPU backend instead")
