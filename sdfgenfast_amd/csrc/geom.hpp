@@ -207,11 +207,6 @@ SDF_HD float ptd_nb(f3 x0, f3 x1, f3 x2, f3 x3)
     return inside ? d_in : d_edge;
 }
 
-// ptd_nb for a wave evaluating many (point, triangle) pairs at once: the inside-projection
-// block and the two-segment block each run only if some active lane needs it (wave-uniform
-// branches).  Every lane still performs exactly ptd_nb's operations for the case it takes,
-// so the result is bit-identical; away from the surface (points project outside the tiny
-// triangles) whole waves skip the inside block.
 // The triangle-only reciprocal of ptd's barycentric solve, exactly as ptd computes it.  The
 // device kernels take it precomputed (k_prep_soup stores it in the third vertex's w), which
 // takes a division off every distance's dependency chain.
@@ -220,36 +215,6 @@ SDF_HD float tri_invdet(f3 x1, f3 x2, f3 x3)
     const f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3);
     const float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
     return div_rn(1.0f, fmax_std(m13 * m23 - d * d, 1e-30f));
-}
-
-__device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3, float invdet)
-{
-    f3 x13 = sub3(x1, x3), x23 = sub3(x2, x3), x03 = sub3(x0, x3);
-    float m13 = mag2(x13), m23 = mag2(x23), d = dot3(x13, x23);
-    float a = dot3(x13, x03), b = dot3(x23, x03);
-    float w23 = invdet * (m23 * a - d * b);
-    float w31 = invdet * (m13 * b - d * a);
-    float w12 = (1.0f - w23) - w31;
-    const bool inside = (w23 >= 0.0f) & (w31 >= 0.0f) & (w12 >= 0.0f);
-    // One sqrt for all branches: the reference returns sqrt(inside) or min(sqrt(e1), sqrt(e2));
-    // a correctly rounded sqrt is monotone, so min(sqrt(e1), sqrt(e2)) == sqrt(min(e1, e2)) bit
-    // for bit (with std::min's argument order, NaN included; squared sums are never -0).
-    float r2 = 0.0f;
-    if (__any(inside)) {
-        f3 p = mk3((x1.x * w23 + x2.x * w31) + x3.x * w12,
-                   (x1.y * w23 + x2.y * w31) + x3.y * w12,
-                   (x1.z * w23 + x2.z * w31) + x3.z * w12);
-        const f3 dd = sub3(x0, p);
-        r2 = (dd.x * dd.x + dd.y * dd.y) + dd.z * dd.z;
-    }
-    if (__any(!inside)) {
-        const bool c23 = w23 > 0.0f, c31 = !c23 & (w31 > 0.0f);
-        const f3 fb = (c23 | c31) ? x2 : x3;
-        const f3 sa = c23 ? x1 : x2;
-        const float e2 = fmin_std(psd_sq(x0, x1, fb), psd_sq(x0, sa, x3));
-        r2 = inside ? r2 : e2;
-    }
-    return sqrt_rn(r2);
 }
 
 // Two point-triangle distances per lane in packed FP32 (v_pk_mul_f32 / v_pk_add_f32: each
@@ -289,6 +254,50 @@ __device__ __forceinline__ f2v psd2(f3x2 x0, f3x2 x1, f3x2 x2)
     const f3x2 p = f3x2{x1.x * s12 + x2.x * w, x1.y * s12 + x2.y * w, x1.z * s12 + x2.z * w};
     const f3x2 d = sub3x2(x0, p);
     return (d.x * d.x + d.y * d.y) + d.z * d.z;   // squared (see ptd_wave: one sqrt at the end)
+}
+
+// ptd_nb for a wave evaluating many (point, triangle) pairs at once: the inside-projection
+// block and the two-segment block each run only if some active lane needs it (wave-uniform
+// branches).  Every lane still performs exactly ptd_nb's operations for the case it takes,
+// so the result is bit-identical; away from the surface (points project outside the tiny
+// triangles) whole waves skip the inside block.
+// ONE point-triangle distance per lane, with the independent halves of its arithmetic paired in
+// packed FP32: (x13 | x23), (m13 | m23), (a | b), (w23 | w31), the inside point's (x | y), and the
+// two edge distances (first | second segment) as one psd2.  Every half performs exactly ptd_nb's
+// operation on the same operands, so the bits are ptd_nb's; the step's chain of one evaluation is
+// 168 instead of 211 VALU (gfx950 ISA).
+__device__ __forceinline__ float ptd_wave(f3 x0, f3 x1, f3 x2, f3 x3, float invdet)
+{
+    const f3x2 X = sub3x2(mk3x2(x1, x2), mk3x2(x3, x3));      // {x13, x23}
+    const f3x2 X03 = sub3x2(mk3x2(x0, x0), mk3x2(x3, x3));    // {x03, x03}
+    const f2v M = mag2x2(X);                                  // {m13, m23}
+    const float d = dot3(f3{X.x.x, X.y.x, X.z.x}, f3{X.x.y, X.y.y, X.z.y});   // dot(x13, x23)
+    const f2v AB = dot3x2(X, X03);                            // {a, b}
+    const f2v T = f2v{M.y, M.x} * AB - f2v{d, d} * f2v{AB.y, AB.x};   // {m23 a - d b, m13 b - d a}
+    const f2v W = f2v{invdet, invdet} * T;                    // {w23, w31}
+    const float w23 = W.x, w31 = W.y;
+    const float w12 = (1.0f - w23) - w31;
+    const bool inside = (w23 >= 0.0f) & (w31 >= 0.0f) & (w12 >= 0.0f);
+    // One sqrt for all branches: the reference returns sqrt(inside) or min(sqrt(e1), sqrt(e2));
+    // a correctly rounded sqrt is monotone, so min(sqrt(e1), sqrt(e2)) == sqrt(min(e1, e2)) bit
+    // for bit (with std::min's argument order, NaN included; squared sums are never -0).
+    float r2 = 0.0f;
+    if (__any(inside)) {
+        const f2v pxy = (f2v{x1.x, x1.y} * w23 + f2v{x2.x, x2.y} * w31) + f2v{x3.x, x3.y} * w12;
+        const float pz = (x1.z * w23 + x2.z * w31) + x3.z * w12;
+        const f2v dxy = f2v{x0.x, x0.y} - pxy;
+        const float dz = x0.z - pz;
+        const f2v sq = dxy * dxy;
+        r2 = (sq.x + sq.y) + dz * dz;
+    }
+    if (__any(!inside)) {
+        const bool c23 = w23 > 0.0f, c31 = !c23 & (w31 > 0.0f);
+        const f3 fb = (c23 | c31) ? x2 : x3;
+        const f3 sa = c23 ? x1 : x2;
+        const f2v e = psd2(mk3x2(x0, x0), mk3x2(x1, sa), mk3x2(fb, x3));   // {psd(x1, fb), psd(sa, x3)}
+        r2 = inside ? r2 : fmin_std(e.x, e.y);
+    }
+    return sqrt_rn(r2);
 }
 __device__ __forceinline__ void ptd_wave2(f3 x0a, f3 x1a, f3 x2a, f3 x3a, float inva, f3 x0b, f3 x1b, f3 x2b, f3 x3b,
                                           float invb, float &da, float &db)
