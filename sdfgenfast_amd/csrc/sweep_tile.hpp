@@ -1446,10 +1446,16 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
                 return fail(-4, "memset");
             W.cap_mtasks = std::max(ntasks, 1);
         }
-        if (ntasks && (hipMemcpyAsync(W.mtasks, mt.data(), ntasks * sizeof(int4), hipMemcpyHostToDevice, st) != hipSuccess ||
-                       hipMemcpyAsync(W.mdeps, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess ||
-                       hipStreamSynchronize(st) != hipSuccess))
-            return fail(-4, "task graph upload");
+        if (ntasks) {
+            hipError_t e = hipMemcpyAsync(W.mtasks, mt.data(), ntasks * sizeof(int4), hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(W.mdeps, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) {
+                char m[96];
+                snprintf(m, sizeof(m), "task graph upload: %s", hipGetErrorName(e));
+                return fail(-4, m);
+            }
+        }
         W.mkey = key;
     }
     if (prepare_only) return 0;   // buffers and tables in place (Z-slabs: before anything is enqueued)
