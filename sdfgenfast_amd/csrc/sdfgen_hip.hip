@@ -539,8 +539,6 @@ struct Workspace {
     SparseSweepWorkspace sp;
     float *out = nullptr;               // phi of the host-buffer entry point before its copy-out
     size_t cap_out = 0;
-    float *stage = nullptr;             // pinned, mapped: the staged copy-out's two slots (run_pipeline)
-    size_t cap_stage = 0;               // floats
 };
 
 std::mutex g_mu;
@@ -622,29 +620,10 @@ int check_oob(Err &err, const char *where)
     return 0;
 }
 
-// Staged copy-out of the host entry point (tools/d2h_probe.py, tools/pcie_write.hip).
-// Under ROCm 7.2 a pageable device-to-host hipMemcpy below the runtime's own pinning threshold goes
-// through its copy engine at ~29 GB/s on MI355X, while kernel stores into pinned host memory cross
-// PCIe at ~53 GB/s and the host copies memory at ~80 GB/s.  So the sign pass writes chunks of planes
-// into two pinned, mapped slots and the host copies chunk c into the caller's array while the GPU
-// signs chunk c + 1.  Above SDFGEN_STAGE_MAX_MB (default 128 MB of phi) the runtime's own copy pins
-// the caller's buffer and is as fast; the k-fastest layout (rows strided by nk) keeps the one copy.
-// SDFGEN_HOST_STAGE=0 turns it off (A/B).  The caller's memory is never registered with HIP.
-constexpr size_t STAGE_CHUNK_BYTES = (size_t)16 << 20;
-inline bool stage_out_wanted(int ni, int nj, int nk, int layout)
-{
-    if (layout != SDFGEN_LAYOUT_ARRAY3) return false;
-    const char *e = getenv("SDFGEN_HOST_STAGE");
-    if (e && atoi(e) == 0) return false;
-    const char *m = getenv("SDFGEN_STAGE_MAX_MB");
-    return 4.0 * ni * nj * nk <= (m ? atof(m) : 128.0) * 1048576.0;
-}
-
-// The whole pipeline on device buffers already resident on ws->device.  With h_out (host entry point,
-// stage_out_wanted) phi goes to the caller's host array through the staged copy-out instead of d_out.
+// The whole pipeline on device buffers already resident on ws->device.
 int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,
                  uint64_t nvert, const float origin[3], float dx, int ni, int nj, int nk, int band, int layout,
-                 float *d_out, Err &err, float *h_out = nullptr)
+                 float *d_out, Err &err)
 {
     const uint64_t n = (uint64_t)ni * nj * nk;
     int rc;
@@ -790,39 +769,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[19], st));
-    if (h_out) {
-        const size_t plane = (size_t)ni * nj;
-        const char *ck = getenv("SDFGEN_STAGE_CHUNK_KB");   // tests: many chunks on a small grid
-        const size_t chunk_b = ck ? (size_t)std::max(1, atoi(ck)) << 10 : STAGE_CHUNK_BYTES;
-        const int kc = (int)std::max<size_t>(1, std::min<size_t>((size_t)nk, chunk_b / (4 * plane)));
-        const int nch = (nk + kc - 1) / kc;
-        const size_t slot = (size_t)kc * plane;   // floats per slot
-        if (ws->cap_stage < 2 * slot) {
-            if (ws->stage) HIPCHK(hipHostFree(ws->stage));
-            ws->stage = nullptr;
-            ws->cap_stage = 0;
-            HIPCHK(hipHostMalloc((void **)&ws->stage, 2 * slot * sizeof(float), hipHostMallocMapped | hipHostMallocCoherent));
-            ws->cap_stage = 2 * slot;
-        }
-        float *dstage = nullptr;
-        HIPCHK(hipHostGetDevicePointer((void **)&dstage, ws->stage, 0));
-        auto launch = [&](int c) -> int {
-            const int k0 = c * kc, cnt = std::min(kc, nk - k0);
-            hipLaunchKernelGGL(k_sign, dim3(grid_for((uint64_t)nj * cnt * 64, 256, 65536)), dim3(256), 0, st, ws->cell,
-                               ws->cnt, g, (int)SDFGEN_LAYOUT_ARRAY3, dstage + (c & 1) * slot, k0, cnt);
-            HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev[30 + (c & 1)], st));
-            return 0;
-        };
-        for (int c = 0; c < std::min(nch, 2); ++c)
-            if ((rc = launch(c))) return rc;
-        for (int c = 0; c < nch; ++c) {   // chunk c leaves while the GPU signs c + 1; c + 2 reuses c's slot
-            HIPCHK(hipEventSynchronize(ev[30 + (c & 1)]));
-            const int k0 = c * kc, cnt = std::min(kc, nk - k0);
-            memcpy(h_out + (size_t)k0 * plane, ws->stage + (c & 1) * slot, (size_t)cnt * plane * sizeof(float));
-            if (c + 2 < nch && (rc = launch(c + 2))) return rc;
-        }
-    } else {
+    {
         const uint64_t rows = (uint64_t)nj * nk;
         if (layout == SDFGEN_LAYOUT_KFAST)
             hipLaunchKernelGGL(k_sign_kfast, dim3(grid_for((uint64_t)nj * ((nk + 63) / 64), 1, 65536)), dim3(256), 0, st,
@@ -1553,18 +1500,19 @@ int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *
     const uint64_t n = (uint64_t)ni * nj * nk;
     if ((rc = grow(&ws->tri, &ws->cap_tri, std::max<uint64_t>(3 * ntri, 1), err))) return rc;
     if ((rc = grow(&ws->xyz, &ws->cap_xyz, std::max<uint64_t>(3 * nvert, 1), err))) return rc;
+    if ((rc = grow(&ws->out, &ws->cap_out, n, err))) return rc;
+    float *d_out = ws->out;
     hipStream_t st = ws->stream;
     if (ntri) {
         HIPCHK(hipMemcpyAsync(ws->tri, tri, 3 * ntri * sizeof(uint32_t), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(ws->xyz, xyz, 3 * nvert * sizeof(float), hipMemcpyHostToDevice, st));
     }
-    // phi leaves through run_pipeline's staged copy-out when it takes it (h_out), else one hipMemcpy
-    const bool staged = stage_out_wanted(ni, nj, nk, out_layout);
-    if (!staged && (rc = grow(&ws->out, &ws->cap_out, n, err))) return rc;
-    rc = run_pipeline(ws, st, ws->tri, ntri, ws->xyz, nvert, origin, dx, ni, nj, nk, exact_band, out_layout,
-                      staged ? nullptr : ws->out, err, staged ? phi_out : nullptr);
-    if (rc == 0 && !staged) {
-        hipError_t e = hipMemcpyAsync(phi_out, ws->out, n * sizeof(float), hipMemcpyDeviceToHost, st);
+    rc = run_pipeline(ws, st, ws->tri, ntri, ws->xyz, nvert, origin, dx, ni, nj, nk, exact_band, out_layout, d_out,
+                      err);
+    if (rc == 0) {
+        // a pageable copy: its cost here is mostly first-touch page faults of the caller's
+        // fresh buffer (a pinned, 8-thread staged copy-out measured no faster)
+        hipError_t e = hipMemcpyAsync(phi_out, d_out, n * sizeof(float), hipMemcpyDeviceToHost, st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) rc = err.set(SDFGEN_HIP_ERUNTIME, "GPU (HIP) error %s copying phi", hipGetErrorName(e));
     }
@@ -1618,7 +1566,6 @@ int sdfgen_hip_release(void)
         hipFree(w->evals);
         hipFree(w->status);
         hipFree(w->out);
-        if (w->stage) hipHostFree(w->stage);
         tile_sweep_release(w->wf);
         sparse_sweep_release(w->sp);
         for (auto &e : w->ev) hipEventDestroy(e);

@@ -245,28 +245,33 @@ def test_gpu_sweep_impls_agree_with_oracle(sweep_impl, nu, nv, dims):
     assert bits_equal(got, want), diff_report(got, want, dx)
 
 
-# ---------------------------------------------------------------- host entry point over PCIe
+# ---------------------------------------------------------------- host entry point
 @pytest.mark.parametrize("layout", [_lib.LAYOUT_ARRAY3, _lib.LAYOUT_KFAST])
-def test_gpu_host_staged_copy_out_matches_reference_digest(monkeypatch, layout):
-    """sdfgen_hip_make_level_set3's staged copy-out (the sign pass storing chunks of planes into two
-    pinned slots, the host copying chunk c out while the GPU signs c + 1) against the one-hipMemcpy
-    path (SDFGEN_HOST_STAGE=0): the reference's bits with one chunk, with 2 and with 32 chunks (slot
-    reuse), into an output array 4 bytes off its allocation's alignment.  The k-fastest layout always
-    takes the copy."""
+def test_gpu_host_entry_into_offset_and_pinned_arrays(layout):
+    """sdfgen_hip_make_level_set3 into an output array 4 bytes off its allocation's alignment and
+    into HIP-pinned host memory (hipHostMalloc, like a pinned torch tensor), from read-only inputs:
+    the reference's bits."""
+    import ctypes
     db = _hashes()
     name = "c2_sphere70k_128"
     if name not in db:
         pytest.skip(f"{name}: no reference digest recorded")
     v, t, o, dx, dims = meshgen.workload(name)
+    v.setflags(write=False)
+    t.setflags(write=False)
     n = dims[0] * dims[1] * dims[2]
-    plane_kb = 4 * dims[0] * dims[1] // 1024
-    for stage, chunk_kb in (("0", None), ("1", None), ("1", plane_kb * dims[2] // 2), ("1", plane_kb * 4)):
-        monkeypatch.setenv("SDFGEN_HOST_STAGE", stage)
-        if chunk_kb:
-            monkeypatch.setenv("SDFGEN_STAGE_CHUNK_KB", str(chunk_kb))
-        else:
-            monkeypatch.delenv("SDFGEN_STAGE_CHUNK_KB", raising=False)
-        for off in (0, 1):
-            out = np.empty(n + 1, np.float32)[off:off + n]
-            got = _lib.make_level_set3(v, t, o, dx, *dims, 1, layout, out=out)
-            assert _hash_i_fastest(got) == db[name]["sha256_phi"], f"stage {stage}, chunk {chunk_kb} KB, offset {4 * off} B"
+    for off in (0, 1):
+        out = np.empty(n + 1, np.float32)[off:off + n]
+        got = _lib.make_level_set3(v, t, o, dx, *dims, 1, layout, out=out)
+        assert _hash_i_fastest(got) == db[name]["sha256_phi"], f"offset {4 * off} B"
+    rt = _hip_runtime()
+    rt.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    rt.hipHostFree.argtypes = [ctypes.c_void_p]
+    p = ctypes.c_void_p()
+    assert rt.hipHostMalloc(ctypes.byref(p), 4 * n, 0) == 0
+    try:
+        out = np.ctypeslib.as_array((ctypes.c_float * n).from_address(p.value))
+        got = _lib.make_level_set3(v, t, o, dx, *dims, 1, layout, out=out)
+        assert _hash_i_fastest(got) == db[name]["sha256_phi"], "pinned output"
+    finally:
+        rt.hipHostFree(p)
