@@ -691,7 +691,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         const char *e = getenv("SDFGEN_SPARSE_WORKERS");   // diagnostics: repair-kernel workgroups
         // repair workgroups: fewer on small grids (256^3: 64 beat 128 by 0.25 ms; 512^3: 128
         // beat 64 by 2.2 ms -- more concurrent chains there)
-        ws->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
+        ws->sp.workers = e ? atoi(e) : sp_workers_for((unsigned long long)ni * nj * nk);
         const char *b = getenv("SDFGEN_SPARSE_BRICK");    // 1 = the brick-owned repair (measured slower)
         ws->sp.brick = b && atoi(b) == 1;
         const char *ip = getenv("SDFGEN_SPARSE_INPLACE");  // diagnostics: 0 = two buffers, swapped per sweep
@@ -1208,7 +1208,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
         // values) unless SDFGEN_SPARSE_INPLACE=0: then the state alternates between cell and alt
         {
             const char *e = getenv("SDFGEN_SPARSE_WORKERS");
-            S->sp.workers = e ? atoi(e) : SP_WORKERS_DEFAULT;
+            S->sp.workers = e ? atoi(e) : sp_workers_for((unsigned long long)ni * nj * (S->k_end - S->k_begin));
             const char *ip = getenv("SDFGEN_SPARSE_INPLACE");
             S->sp.inplace = !(ip && atoi(ip) == 0);
         }

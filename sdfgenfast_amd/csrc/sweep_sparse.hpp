@@ -74,6 +74,9 @@ constexpr unsigned long long SP_TAIL_LIMIT = 0xF0000000ull;   // appends per swe
 constexpr unsigned SP_WATCHDOG = 1u << 24;   // empty polls (~1 s) before giving up
 constexpr int SP_WORKERS = 512;              // max one-wave workgroups of the repair kernel
 constexpr int SP_WORKERS_DEFAULT = 256;   // 64-thread repair workgroups (C3: 64 -> 4.75 ms, 256 -> 4.6; C4: 128 -> 21.2, 256 -> 19.5)
+// Repair workgroups for a repair over n cells: 512 above 2^25 cells (C4 second pass 12.9-13.1 ->
+// 12.2-12.4 ms, more concurrent change chains; C3 neutral: profiles/r03_ab_workers_c{3,4}.log)
+inline int sp_workers_for(unsigned long long n) { return n > (1ull << 25) ? SP_WORKERS : SP_WORKERS_DEFAULT; }
 #ifndef SP_NQ
 #define SP_NQ 8        // work-list shards (fewer where NQ rings of n cells would pass 2^31 entries)
 #endif
