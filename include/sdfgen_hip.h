@@ -214,6 +214,15 @@ int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, 
 int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *out4,
                            char *errbuf, size_t errlen);
 
+/* Diagnostics (used by the parity tests): stage 1 only -- init, narrow band and ray-parity counts
+ * (cpu_lib/makelevelset3.cpp:196-236) -- on the current device, host buffers in and the pre-sweep
+ * state out: phi and closest_tri (-1 = none) per cell and the intersection counts, i-fastest, each
+ * ni*nj*nk entries.  *big_n (if not NULL) = triangles the band phase spread over the chip as big
+ * ones (band box > 4096 cells or ray lattice > 1024 points). */
+int sdfgen_hip_debug_band(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert, const float origin[3],
+                          float dx, int ni, int nj, int nk, int exact_band, float *phi, int32_t *ct, uint32_t *cnt,
+                          uint64_t *big_n, char *errbuf, size_t errlen);
+
 /* Diagnostics: per-task [start, first step, middle step, end] wall-clock stamps (100 MHz) of the sweep named by
  * the SDFGEN_TRACE_SWEEP environment variable in the last call (tasks in dequeue order). */
 int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries, uint64_t *n_out);

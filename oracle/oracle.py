@@ -53,6 +53,8 @@ def lib():
         L.oracle_band.argtypes = [_P, ctypes.c_uint64, _P, ctypes.c_uint64, _P, ctypes.c_float,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P, _P, _P]
         L.oracle_band.restype = ctypes.c_int
+        L.oracle_band_mt.argtypes = L.oracle_band.argtypes + [ctypes.c_int]
+        L.oracle_band_mt.restype = ctypes.c_int
         L.oracle_sweep.argtypes = [_P, _P, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    _P, _P, ctypes.c_int]
         L.oracle_sweep.restype = None
@@ -118,6 +120,24 @@ def band(vertices, triangles, origin, dx, ni, nj, nk, exact_band=1):
                            ni, nj, nk, exact_band, _ptr(phi), _ptr(ct), _ptr(cnt))
     if rc != 0:
         raise ValueError(f"oracle_band failed rc={rc}")
+    f = lambda a: a.reshape((ni, nj, nk), order="F")
+    return f(phi), f(ct), f(cnt)
+
+
+def band_mt(vertices, triangles, origin, dx, ni, nj, nk, exact_band=1, threads=None):
+    """Stage 1 split over host threads by planes (oracle_band_mt) -- bit-identical to band();
+    for parity cases with billions of band evaluations."""
+    v, t, o = _prep(vertices, triangles, origin)
+    n = ni * nj * nk
+    phi = np.empty(n, np.float32)
+    ct = np.empty(n, np.int32)
+    cnt = np.empty(n, np.int32)
+    if threads is None:
+        threads = max(1, min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "64") or 64)))
+    rc = lib().oracle_band_mt(_ptr(t), t.shape[0], _ptr(v), v.shape[0], _ptr(o), ctypes.c_float(dx),
+                              ni, nj, nk, exact_band, _ptr(phi), _ptr(ct), _ptr(cnt), int(threads))
+    if rc != 0:
+        raise ValueError(f"oracle_band_mt failed rc={rc}")
     f = lambda a: a.reshape((ni, nj, nk), order="F")
     return f(phi), f(ct), f(cnt)
 

@@ -21,6 +21,7 @@
  * oracle/Makefile (target _ref) -- see tests/golden/make_golden.py.
  */
 #include <math.h>
+#include <pthread.h>
 #include <stddef.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -196,6 +197,102 @@ int oracle_band(const uint32_t *tri, uint64_t ntri, const float *x, uint64_t nve
                 }
             }
     }
+    return 0;
+}
+
+/*
+ * Stage 1 again, split over host threads by planes: thread r fills k in [k_lo, k_hi) and runs
+ * EVERY triangle in ascending t over those planes only.  A cell sees the same triangles in the
+ * same order as in oracle_band (the band boxes and ray lattices are the reference's whole-grid
+ * boxes, cut to the planes afterwards), so phi / ct / cnt are bit-identical -- pinned against
+ * oracle_band by tests/test_oracle_golden.py.  For big parity cases (> 2^32 band evaluations).
+ * phi, ct and cnt must be initialised by the caller (oracle_band_mt does it).
+ */
+typedef struct {
+    const uint32_t *tri; uint64_t ntri; const float *x; const float *origin; float dx;
+    int ni, nj, nk, exact_band, k_lo, k_hi; float *phi; int32_t *ct; int32_t *cnt;
+} band_job;
+
+static void band_planes(const band_job *J)
+{
+    const float *origin = J->origin;
+    const float dx = J->dx;
+    const int ni = J->ni, nj = J->nj, nk = J->nk, exact_band = J->exact_band;
+    for (uint64_t t = 0; t < J->ntri; ++t) {
+        const float *xp = J->x + 3 * (size_t)J->tri[3 * t + 0];
+        const float *xq = J->x + 3 * (size_t)J->tri[3 * t + 1];
+        const float *xr = J->x + 3 * (size_t)J->tri[3 * t + 2];
+        double fip = ((double)xp[0] - origin[0]) / dx, fjp = ((double)xp[1] - origin[1]) / dx, fkp = ((double)xp[2] - origin[2]) / dx;
+        double fiq = ((double)xq[0] - origin[0]) / dx, fjq = ((double)xq[1] - origin[1]) / dx, fkq = ((double)xq[2] - origin[2]) / dx;
+        double fir = ((double)xr[0] - origin[0]) / dx, fjr = ((double)xr[1] - origin[1]) / dx, fkr = ((double)xr[2] - origin[2]) / dx;
+        int i0 = clampi(wrap_add(trunc_to_int(dmin3(fip, fiq, fir)), -exact_band), 0, ni - 1);
+        int i1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fip, fiq, fir)), exact_band), 1), 0, ni - 1);
+        int j0 = clampi(wrap_add(trunc_to_int(dmin3(fjp, fjq, fjr)), -exact_band), 0, nj - 1);
+        int j1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fjp, fjq, fjr)), exact_band), 1), 0, nj - 1);
+        int k0 = clampi(wrap_add(trunc_to_int(dmin3(fkp, fkq, fkr)), -exact_band), 0, nk - 1);
+        int k1 = clampi(wrap_add(wrap_add(trunc_to_int(dmax3(fkp, fkq, fkr)), exact_band), 1), 0, nk - 1);
+        if (k0 < J->k_lo) k0 = J->k_lo;
+        if (k1 > J->k_hi - 1) k1 = J->k_hi - 1;
+        for (int k = k0; k <= k1; ++k)
+            for (int j = j0; j <= j1; ++j)
+                for (int i = i0; i <= i1; ++i) {
+                    float gx[3] = {(float)i * dx + origin[0], (float)j * dx + origin[1], (float)k * dx + origin[2]};
+                    float d = oracle_ptd(gx, xp, xq, xr);
+                    size_t q = cidx(i, j, k, ni, nj);
+                    if (d < J->phi[q]) { J->phi[q] = d; J->ct[q] = (int32_t)t; }
+                }
+        j0 = clampi(trunc_to_int(ceil(dmin3(fjp, fjq, fjr))), 0, nj - 1);
+        j1 = clampi(trunc_to_int(floor(dmax3(fjp, fjq, fjr))), 0, nj - 1);
+        k0 = clampi(trunc_to_int(ceil(dmin3(fkp, fkq, fkr))), 0, nk - 1);
+        k1 = clampi(trunc_to_int(floor(dmax3(fkp, fkq, fkr))), 0, nk - 1);
+        if (k0 < J->k_lo) k0 = J->k_lo;
+        if (k1 > J->k_hi - 1) k1 = J->k_hi - 1;
+        for (int k = k0; k <= k1; ++k)
+            for (int j = j0; j <= j1; ++j) {
+                double a, b, c;
+                if (oracle_pit2d((double)j, (double)k, fjp, fkp, fjq, fkq, fjr, fkr, &a, &b, &c)) {
+                    double fi = (a * fip + b * fiq) + c * fir;
+                    int ii = trunc_to_int(ceil(fi));
+                    if (ii < 0) ++J->cnt[cidx(0, j, k, ni, nj)];
+                    else if (ii < ni) ++J->cnt[cidx(ii, j, k, ni, nj)];
+                }
+            }
+    }
+}
+
+static void *band_thread(void *arg)
+{
+    band_planes((const band_job *)arg);
+    return NULL;
+}
+
+int oracle_band_mt(const uint32_t *tri, uint64_t ntri, const float *x, uint64_t nvert,
+                   const float origin[3], float dx, int ni, int nj, int nk, int exact_band,
+                   float *phi, int32_t *ct, int32_t *cnt, int nthreads)
+{
+    int rc = check_args(tri, ntri, nvert, ni, nj, nk);
+    if (rc) return rc;
+    size_t n = (size_t)ni * nj * nk;
+    float init = (float)(ni + nj + nk) * dx;
+    for (size_t q = 0; q < n; ++q) { phi[q] = init; ct[q] = -1; cnt[q] = 0; }
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > nk) nthreads = nk;
+    if (nthreads > 256) nthreads = 256;
+    band_job jobs[256];
+    pthread_t th[256];
+    for (int r = 0; r < nthreads; ++r) {
+        band_job J = {tri, ntri, x, origin, dx, ni, nj, nk, exact_band,
+                      (int)((int64_t)nk * r / nthreads), (int)((int64_t)nk * (r + 1) / nthreads), phi, ct, cnt};
+        jobs[r] = J;
+    }
+    int started = 0;
+    for (int r = 1; r < nthreads; ++r) {
+        if (pthread_create(&th[r], NULL, band_thread, &jobs[r]) != 0) break;
+        started = r;
+    }
+    band_planes(&jobs[0]);
+    for (int r = started + 1; r < nthreads; ++r) band_planes(&jobs[r]);   /* threads that failed to start */
+    for (int r = 1; r <= started; ++r) pthread_join(th[r], NULL);
     return 0;
 }
 

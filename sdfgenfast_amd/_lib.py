@@ -34,6 +34,7 @@ EXPORTED = (
     "sdfgen_hip_release",
     "sdfgen_hip_debug_ptd",
     "sdfgen_hip_debug_pit2d",
+    "sdfgen_hip_debug_band",
     "sdfgen_cpu_make_level_set3",
     "sdfgen_hip_debug_sweep_trace",
     "sdfgen_hip_slab_create",
@@ -131,6 +132,11 @@ def _load():
     L.sdfgen_hip_debug_ptd.restype = ctypes.c_int
     L.sdfgen_hip_debug_pit2d.argtypes = [ctypes.c_int, _u64, _P, _P, ctypes.c_char_p, ctypes.c_size_t]
     L.sdfgen_hip_debug_pit2d.restype = ctypes.c_int
+    if hasattr(L, "sdfgen_hip_debug_band"):   # (absent from A/B builds of older sources)
+        L.sdfgen_hip_debug_band.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, _P, _P, _P, ctypes.POINTER(_u64),
+                                            ctypes.c_char_p, ctypes.c_size_t]
+        L.sdfgen_hip_debug_band.restype = ctypes.c_int
     L.sdfgen_hip_debug_sweep_trace.argtypes = [ctypes.c_int, _P, _u64, ctypes.POINTER(_u64)]
     L.sdfgen_hip_debug_sweep_trace.restype = ctypes.c_int
     _E = [ctypes.c_char_p, ctypes.c_size_t]
@@ -300,6 +306,27 @@ def debug_ptd(pts: np.ndarray, device: int = 0, variant: int = 0) -> np.ndarray:
     if rc != OK:
         _raise(rc, err)
     return out
+
+
+def debug_band(vertices, triangles, origin, dx: float, ni: int, nj: int, nk: int, exact_band: int = 1):
+    """Stage 1 only on the current device (sdfgen_hip_debug_band) -> (phi, closest_tri, counts, big_n):
+    the pre-sweep state as (ni,nj,nk) Fortran-ordered views of the i-fastest buffers (the layout of
+    oracle.band), and the number of triangles the band phase treated as big."""
+    v = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 3)
+    t = np.ascontiguousarray(triangles, dtype=np.uint32).reshape(-1, 3)
+    o = np.ascontiguousarray(np.asarray(origin, dtype=np.float32).reshape(3))
+    n = int(ni) * int(nj) * int(nk)
+    phi, ct, cnt = np.empty(n, np.float32), np.empty(n, np.int32), np.empty(n, np.uint32)
+    big = _u64(0)
+    err = ctypes.create_string_buffer(512)
+    rc = lib.sdfgen_hip_debug_band(t.ctypes.data_as(_P), t.shape[0], v.ctypes.data_as(_P), v.shape[0],
+                                   o.ctypes.data_as(_P), ctypes.c_float(dx), int(ni), int(nj), int(nk),
+                                   int(exact_band), phi.ctypes.data_as(_P), ct.ctypes.data_as(_P),
+                                   cnt.ctypes.data_as(_P), ctypes.byref(big), err, ctypes.sizeof(err))
+    if rc != OK:
+        _raise(rc, err)
+    f = lambda a: a.reshape((ni, nj, nk), order="F")
+    return f(phi), f(ct), f(cnt), int(big.value)
 
 
 def debug_sweep_trace(device: int = 0, max_entries: int = 1 << 22) -> np.ndarray:

@@ -133,14 +133,23 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
     return (size_t)i + (size_t)ni * ((size_t)j + (size_t)nj * (size_t)k);
 }
 
-// Band + ray parity for batches of BT consecutive triangles per workgroup (:203-236).
-// Consecutive triangles of a mesh are usually neighbours, so their band boxes overlap:
-// the batch's candidates are first merged per cell in LDS (ds_min_u64 on the same
-// (f32bits(d) << 32 | t) keys), and only the union box's winners go to HBM with one
-// global atomicMin each -- about 5x fewer global atomics than one per (triangle, cell).
-// A batch whose union box does not fit the LDS table falls back to direct global
-// atomics.  min() is order-independent, so the result is the one-triangle-at-a-time
-// result bit for bit.
+// ---------------------------------------------------------------------------
+// Narrow band + ray parity (:203-236).
+//
+// Two work classes, so that no workgroup ever holds more than a bounded amount of work and no
+// count can wrap (triangle boxes reach 2^30 cells at 1024^3, and a batch of them 2^36):
+//   * small triangles (band box <= BAND_BIG_VOL cells and ray lattice <= BAND_BIG_LAT points) --
+//     the sub-cell triangles of a fine mesh -- in batches of BAND_BT consecutive triangles per
+//     workgroup (k_band_lds): the batch's (triangle, cell) pairs flattened over 256 threads,
+//     candidates merged per cell in LDS (ds_min_u64 on (f32bits(d) << 32 | t)) and one global
+//     atomicMin per cell of the union box; the batch's ray-lattice points flattened the same way;
+//   * big triangles -- coarse meshes, a wide exact_band, grid-spanning faces -- are appended to a
+//     list by the batch kernel, a one-workgroup scan turns their chunk counts into 64-bit offsets
+//     (k_band_big_scan), and k_band_big spreads the chunks (BAND_CH_PAIRS cells or BAND_CH_LAT
+//     lattice points of one triangle) over every wave of the chip.
+// min() and the parity counts are order-independent, so the result is the one-triangle-at-a-time
+// result bit for bit whatever runs where.
+// ---------------------------------------------------------------------------
 #ifndef BAND_BT_DEF
 #define BAND_BT_DEF 64   // 64 (with the 40 KB table): band 0.86 -> 0.81 ms at C3; 16: 0.99
 #endif
@@ -150,14 +159,25 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 constexpr int BAND_BT = BAND_BT_DEF;    // triangles per batch (<= 64: one wave sets a batch up)
 constexpr int BAND_LDS = BAND_LDS_DEF;  // u64 keys in the LDS table (40 KB)
 static_assert(BAND_BT >= 1 && BAND_BT <= 64, "a batch's boxes are scanned by one wave");
-// pair_of's binary search halves from BAND_BT / 2: it reaches every triangle only for a power of two
+// find_q's binary search halves from BAND_BT / 2: it reaches every triangle only for a power of two
 // (BAND_BT_DEF=48 measured a digest mismatch at C3: triangle 47 of a batch was never paired)
 static_assert((BAND_BT & (BAND_BT - 1)) == 0, "BAND_BT must be a power of two");
+constexpr uint32_t BAND_BIG_VOL = 4096;    // band-box cells above which a triangle is "big"
+constexpr uint32_t BAND_BIG_LAT = 1024;    // ray-lattice points above which a triangle is "big"
+constexpr uint32_t BAND_CH_PAIRS = 1024;   // cells per big-triangle chunk (one wave: 16 per lane)
+constexpr uint32_t BAND_CH_LAT = 256;      // lattice points per big-triangle chunk (4 per lane)
+// a batch's flattened counts stay far inside 32 bits
+static_assert((uint64_t)BAND_BT * BAND_BIG_VOL < (1ull << 31) && (uint64_t)BAND_BT * BAND_BIG_LAT < (1ull << 31), "");
 
 struct BandBox {
     int i0, j0, k0, bi, bj, bk;         // clamped band box (bi*bj*bk cells; 0 = empty)
 };
+struct LatBox {
+    int j0, k0, nj, nk;                 // clamped ray lattice (nj*nk (j,k) points; 0 = empty)
+};
 
+// Grid coordinates of the triangle's vertices (:206-208) and its band box (:210-212), cut to the
+// slab's planes [k_lo, k_hi) AFTER the reference's whole-grid clamp.
 __device__ __forceinline__ void band_box(const float4 *soup, uint64_t t, const Grid &g, int band, int k_lo, int k_hi,
                                          BandBox &B, double f[9])
 {
@@ -183,57 +203,119 @@ __device__ __forceinline__ void band_box(const float4 *soup, uint64_t t, const G
     B.bk = ok ? k1 - k0 + 1 : 0;
 }
 
+// The ray lattice of :222-225 (its own clamp, independent of the band box: for a NaN, infinite or
+// far vertex the two boxes differ), cut to the slab's planes.
+__device__ __forceinline__ void lat_box(const double f[9], const Grid &g, int k_lo, int k_hi, LatBox &L)
+{
+    const int j0 = clampi(trunc_to_int(ceil(dmin3(f[1], f[4], f[7]))), 0, g.nj - 1);
+    const int j1 = clampi(trunc_to_int(floor(dmax3(f[1], f[4], f[7]))), 0, g.nj - 1);
+    const int k0 = max(clampi(trunc_to_int(ceil(dmin3(f[2], f[5], f[8]))), 0, g.nk - 1), k_lo);
+    const int k1 = min(clampi(trunc_to_int(floor(dmax3(f[2], f[5], f[8]))), 0, g.nk - 1), k_hi - 1);
+    const bool ok = j1 >= j0 && k1 >= k0;
+    L.j0 = j0;
+    L.k0 = k0;
+    L.nj = ok ? j1 - j0 + 1 : 0;
+    L.nk = ok ? k1 - k0 + 1 : 0;
+}
+
+// One lattice point of the ray-parity test (:226-235).
+__device__ __forceinline__ void parity_point(const double *f, int j, int k, const Grid &g, uint32_t *cnt)
+{
+    double a, b, cc;
+    if (pit2d((double)j, (double)k, f[1], f[2], f[4], f[5], f[7], f[8], a, b, cc)) {
+        const double fi = (a * f[0] + b * f[3]) + cc * f[6];
+        const int ii = trunc_to_int(ceil(fi));
+        if (ii < 0) atomicAdd(cnt + cidx(0, j, k, g.ni, g.nj), 1u);
+        else if (ii < g.ni) atomicAdd(cnt + cidx(ii, j, k, g.ni, g.nj), 1u);
+    }
+}
+
+// The big-triangle list of one call: appended by k_band_lds, offsets by k_band_big_scan.
+struct BandBig {
+    uint32_t *tri;      // [cap] triangle index
+    uint32_t *chunks;   // [cap] chunk count (pair chunks, then lattice chunks)
+    u64 *pre;           // [cap + 1] exclusive prefix of chunks; pre[n] = total
+    uint32_t *n;        // entries appended (zeroed per call)
+};
+
+__device__ __forceinline__ uint32_t ceil_div64(uint64_t a, uint32_t b) { return (uint32_t)((a + b - 1) / b); }
+
+// Last q in [0, nb) with pre[q] <= fl (pre ascending, pre[0] = 0).
+__device__ __forceinline__ int find_q(const unsigned *pre, int nb, unsigned fl)
+{
+    int q = 0;
+#pragma unroll
+    for (int step = BAND_BT / 2; step >= 1; step >>= 1)
+        if (q + step < nb && pre[q + step] <= fl) q += step;
+    return q;
+}
+
 __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
                                                   float init, u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
-                                                  unsigned long long *__restrict__ eval_count, int k_lo, int k_hi)
+                                                  unsigned long long *__restrict__ eval_count, int k_lo, int k_hi,
+                                                  BandBig big)
 {
     __shared__ u64 s_key[BAND_LDS];
     __shared__ BandBox s_box[BAND_BT];
+    __shared__ LatBox s_lat[BAND_BT];
+    __shared__ double s_f[BAND_BT][9];        // grid coordinates of the batch's vertices (parity)
     __shared__ unsigned s_pre[BAND_BT + 1];   // prefix sums of the box volumes
+    __shared__ unsigned s_lpre[BAND_BT + 1];  // prefix sums of the lattice sizes
     __shared__ int s_u[6];                    // union box: i0, j0, k0, ni, nj, nk
     const int tid = threadIdx.x;
     unsigned long long evals = 0;
     for (uint64_t t0 = (uint64_t)blockIdx.x * BAND_BT; t0 < ntri; t0 += (uint64_t)gridDim.x * BAND_BT) {
         const int nb = (int)min<uint64_t>(BAND_BT, ntri - t0);
-        double f[9];
-        if (tid < BAND_BT) {
-            BandBox B{0, 0, 0, 0, 0, 0};
-            if (tid < nb) band_box(soup, t0 + tid, g, band, k_lo, k_hi, B, f);
-            s_box[tid] = B;
-            // ray-parity lattice of this triangle (:222-235), one thread per triangle
-            if (tid < nb) {
-                int pj0 = clampi(trunc_to_int(ceil(dmin3(f[1], f[4], f[7]))), 0, g.nj - 1);
-                int pj1 = clampi(trunc_to_int(floor(dmax3(f[1], f[4], f[7]))), 0, g.nj - 1);
-                int pk0 = clampi(trunc_to_int(ceil(dmin3(f[2], f[5], f[8]))), 0, g.nk - 1);
-                int pk1 = clampi(trunc_to_int(floor(dmax3(f[2], f[5], f[8]))), 0, g.nk - 1);
-                pk0 = max(pk0, k_lo);
-                pk1 = min(pk1, k_hi - 1);
-                for (int k = pk0; k <= pk1; ++k)
-                    for (int j = pj0; j <= pj1; ++j) {
-                        double a, b, cc;
-                        if (pit2d((double)j, (double)k, f[1], f[2], f[4], f[5], f[7], f[8], a, b, cc)) {
-                            const double fi = (a * f[0] + b * f[3]) + cc * f[6];
-                            const int ii = trunc_to_int(ceil(fi));
-                            if (ii < 0) atomicAdd(cnt + cidx(0, j, k, g.ni, g.nj), 1u);
-                            else if (ii < g.ni) atomicAdd(cnt + cidx(ii, j, k, g.ni, g.nj), 1u);
-                        }
-                    }
-            }
-        }
         if (tid < 64) {
-            // wave 0: prefix sums of the box volumes and the union box across lanes (lane q =
-            // triangle q; lanes >= nb carry empty boxes) -- no single-thread loop
+            // wave 0, lane q = triangle t0 + q (lanes >= nb carry empty boxes): boxes, the big-triangle
+            // hand-off, prefix sums of the box and lattice sizes and the union box -- no single-thread loop
             BandBox B{0, 0, 0, 0, 0, 0};
-            if (tid < nb) B = s_box[tid];
-            const unsigned vol = (unsigned)(B.bi * B.bj * B.bk);
-            unsigned incl = vol;
+            LatBox L{0, 0, 0, 0};
+            double f[9];
+            if (tid < nb) {
+                band_box(soup, t0 + tid, g, band, k_lo, k_hi, B, f);
+                lat_box(f, g, k_lo, k_hi, L);
+            }
+            const uint64_t vol = (uint64_t)B.bi * (uint64_t)B.bj * (uint64_t)B.bk;
+            const uint64_t lat = (uint64_t)L.nj * (uint64_t)L.nk;
+            const bool is_big = vol > BAND_BIG_VOL || lat > BAND_BIG_LAT;
+            const u64 bm = __ballot(is_big);
+            if (bm) {   // one append per wave
+                uint32_t base = 0;
+                if (tid == __ffsll((long long)bm) - 1) base = atomicAdd(big.n, (uint32_t)__popcll(bm));
+                base = __shfl(base, __ffsll((long long)bm) - 1);
+                if (is_big) {
+                    const uint32_t slot = base + (uint32_t)__popcll(bm & ((1ull << tid) - 1ull));
+                    big.tri[slot] = (uint32_t)(t0 + tid);
+                    big.chunks[slot] = ceil_div64(vol, BAND_CH_PAIRS) + ceil_div64(lat, BAND_CH_LAT);
+                    B = BandBox{0, 0, 0, 0, 0, 0};
+                    L = LatBox{0, 0, 0, 0};
+                }
+            }
+            s_box[tid] = B;
+            s_lat[tid] = L;
+            if (L.nj) {
+#pragma unroll
+                for (int c = 0; c < 9; ++c) s_f[tid][c] = f[c];
+            }
+            const unsigned v32 = (unsigned)(B.bi * B.bj * B.bk), l32 = (unsigned)(L.nj * L.nk);
+            unsigned incl = v32, lincl = l32;
 #pragma unroll
             for (int d = 1; d < 64; d <<= 1) {
-                const unsigned y = __shfl_up(incl, d);
-                if (tid >= d) incl += y;
+                const unsigned y = __shfl_up(incl, d), ly = __shfl_up(lincl, d);
+                if (tid >= d) {
+                    incl += y;
+                    lincl += ly;
+                }
             }
-            if (tid < nb) s_pre[tid] = incl - vol;
-            if (tid == nb - 1) s_pre[nb] = incl;
+            if (tid < nb) {
+                s_pre[tid] = incl - v32;
+                s_lpre[tid] = lincl - l32;
+            }
+            if (tid == nb - 1) {
+                s_pre[nb] = incl;
+                s_lpre[nb] = lincl;
+            }
             int ui0 = B.bi ? B.i0 : INT_MAX, uj0 = B.bi ? B.j0 : INT_MAX, uk0 = B.bi ? B.k0 : INT_MAX;
             int ui1 = B.bi ? B.i0 + B.bi - 1 : -1, uj1 = B.bi ? B.j0 + B.bj - 1 : -1, uk1 = B.bi ? B.k0 + B.bk - 1 : -1;
 #pragma unroll
@@ -249,20 +331,24 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
             }
         }
         __syncthreads();
-        const unsigned total = s_pre[nb];
+        const unsigned total = s_pre[nb], ltotal = s_lpre[nb];
         evals += tid == 0 ? total : 0;
         const int ui0 = s_u[0], uj0 = s_u[1], uk0 = s_u[2], uni = s_u[3], unj = s_u[4];
         const unsigned long long uvol = (unsigned long long)uni * unj * (unsigned)s_u[5];
         const bool merge = uvol > 0 && uvol <= BAND_LDS;
         if (merge)
             for (unsigned c = tid; c < uvol; c += 256) s_key[c] = ~0ull;
+        // the batch's ray-lattice points over all 256 threads (:222-235)
+        for (unsigned fl = tid; fl < ltotal; fl += 256) {
+            const int q = find_q(s_lpre, nb, fl);
+            const LatBox L = s_lat[q];
+            const unsigned r = fl - s_lpre[q], kk = r / (unsigned)L.nj;
+            parity_point(s_f[q], L.j0 + (int)(r - kk * (unsigned)L.nj), L.k0 + (int)kk, g, cnt);
+        }
         __syncthreads();
         // (triangle, cell) pair of flat index fl
         auto pair_of = [&](unsigned fl, int &i, int &j, int &k, uint64_t &t) {
-            int q = 0;   // last q with s_pre[q] <= fl
-#pragma unroll
-            for (int step = BAND_BT / 2; step >= 1; step >>= 1)
-                if (q + step < nb && s_pre[q + step] <= fl) q += step;
+            const int q = find_q(s_pre, nb, fl);
             const BandBox B = s_box[q];
             const unsigned r = fl - s_pre[q], bij = (unsigned)(B.bi * B.bj);
             const unsigned kk = r / bij, rem = r - kk * bij, jj = rem / (unsigned)B.bi;
@@ -313,6 +399,158 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
         __syncthreads();
     }
     if (eval_count && tid == 0 && evals) atomicAdd(eval_count, evals);
+}
+
+// Exclusive prefix of the big triangles' chunk counts in 64 bits (one workgroup; the list holds at
+// most one entry per BAND_BIG_VOL cells or BAND_BIG_LAT lattice points of band work, so this scan
+// is small against the work it dispatches, and empty -- one wave reading one word -- for fine meshes).
+__global__ void __launch_bounds__(1024) k_band_big_scan(BandBig big)
+{
+    __shared__ u64 s_w[16];
+    __shared__ u64 s_carry;
+    const uint32_t n = *big.n;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) s_carry = 0;
+    __syncthreads();
+    for (uint32_t b = 0; b < n; b += 1024) {
+        const uint32_t e = b + tid;
+        const u64 v = e < n ? big.chunks[e] : 0;
+        u64 incl = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const u64 y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+        }
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        u64 wbase = s_carry;
+        for (int q = 0; q < w; ++q) wbase += s_w[q];
+        if (e < n) big.pre[e] = wbase + incl - v;
+        __syncthreads();
+        if (tid == 1023) s_carry = wbase + incl;
+        __syncthreads();
+    }
+    if (tid == 0) big.pre[n] = s_carry;
+}
+
+// The big triangles' chunks, one per wave at a time over the whole chip: chunk c of entry e is
+// BAND_CH_PAIRS consecutive cells of the triangle's band box (c < its pair chunks) or BAND_CH_LAT
+// consecutive points of its ray lattice.  No LDS merge: a big triangle's cells are distinct, and
+// the load-compare keeps the atomics to the cells it improves.
+__global__ void __launch_bounds__(256) k_band_big(const float4 *__restrict__ soup, Grid g, int band, float init,
+                                                  u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
+                                                  unsigned long long *__restrict__ eval_count, int k_lo, int k_hi,
+                                                  BandBig big)
+{
+    const uint32_t n = *big.n;
+    if (n == 0) return;
+    const u64 total = big.pre[n];
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    unsigned long long evals = 0;
+    for (uint64_t q = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); q < total; q += nw) {
+        // entry: the last e with pre[e] <= q, by a 64-ary search across the wave's lanes
+        uint32_t lo = 0, hi = n;
+        while (hi - lo > 1) {
+            const uint32_t step = (hi - lo + 63) / 64, x = lo + (uint32_t)lane * step;
+            const u64 m = __ballot(x < hi && big.pre[x] <= q);   // lanes 0 .. c-1 (pre ascending; lane 0 always)
+            const uint32_t c = (uint32_t)__popcll(m);
+            lo += (c - 1) * step;
+            hi = min(hi, lo + step);
+        }
+        const uint32_t e = lo;
+        const uint64_t t = big.tri[e];
+        BandBox B;
+        LatBox L;
+        double f[9];
+        band_box(soup, t, g, band, k_lo, k_hi, B, f);
+        lat_box(f, g, k_lo, k_hi, L);
+        const uint64_t vol = (uint64_t)B.bi * (uint64_t)B.bj * (uint64_t)B.bk;
+        const uint64_t lat = (uint64_t)L.nj * (uint64_t)L.nk;
+        const uint64_t c = q - big.pre[e];
+        const uint64_t npc = (vol + BAND_CH_PAIRS - 1) / BAND_CH_PAIRS;
+        if (c < npc) {
+            // cells [c * CH, c * CH + CH) of the box, i fastest: decode the chunk start once (64-bit),
+            // then each cell as a small offset from it (32-bit)
+            const uint64_t b0 = c * BAND_CH_PAIRS, bij = (uint64_t)B.bi * (uint64_t)B.bj;
+            const uint32_t rk = (uint32_t)(b0 / bij);
+            const uint64_t rem = b0 - (uint64_t)rk * bij;   // < bi * bj, which may pass 2^32
+            const uint32_t rj = (uint32_t)(rem / (uint64_t)B.bi), ri = (uint32_t)(rem - (uint64_t)rj * B.bi);
+            const uint32_t nvalid = (uint32_t)min<uint64_t>(BAND_CH_PAIRS, vol - b0);
+            evals += lane == 0 ? nvalid : 0;
+            const f3 x1 = load_vtx(soup, t, 0), x2 = load_vtx(soup, t, 1), x3 = load_vtx(soup, t, 2);
+            const float inv = soup[3 * t + 2].w;
+            auto cell_of = [&](uint32_t r, int &i, int &j, int &k) {
+                const uint32_t ii = ri + r, cj = ii / (uint32_t)B.bi;
+                const uint32_t jj = rj + cj, ck = jj / (uint32_t)B.bj;
+                i = B.i0 + (int)(ii - cj * (uint32_t)B.bi);
+                j = B.j0 + (int)(jj - ck * (uint32_t)B.bj);
+                k = B.k0 + (int)(rk + ck);
+            };
+            auto emit = [&](float d, int i, int j, int k) {
+                if (d < init) {   // also rejects NaN
+                    const u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
+                    u64 *p = cell + cidx(i, j, k, g.ni, g.nj);
+                    if (key < *p) atomicMin(p, key);
+                }
+            };
+            for (uint32_t r = lane; r < nvalid; r += 128) {   // two cells per lane in packed FP32
+                const bool two = r + 64 < nvalid;
+                int i, j, k, i2, j2, k2;
+                cell_of(r, i, j, k);
+                cell_of(two ? r + 64 : r, i2, j2, k2);
+                const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
+                const f3 gx2 = mk3((float)i2 * g.dx + g.ox, (float)j2 * g.dx + g.oy, (float)k2 * g.dx + g.oz);
+                float d, d2 = 0.0f;
+                if (__any(two)) ptd_wave2(gx, x1, x2, x3, inv, gx2, x1, x2, x3, inv, d, d2);
+                else d = ptd_wave(gx, x1, x2, x3, inv);
+                emit(d, i, j, k);
+                if (two) emit(d2, i2, j2, k2);
+            }
+        } else {
+            const uint64_t b0 = (c - npc) * BAND_CH_LAT;
+            const uint32_t rk = (uint32_t)(b0 / (uint64_t)L.nj), rj = (uint32_t)(b0 - (uint64_t)rk * L.nj);
+            const uint32_t nvalid = (uint32_t)min<uint64_t>(BAND_CH_LAT, lat - b0);
+            for (uint32_t r = lane; r < nvalid; r += 64) {
+                const uint32_t jj = rj + r, ck = jj / (uint32_t)L.nj;
+                parity_point(f, L.j0 + (int)(jj - ck * (uint32_t)L.nj), L.k0 + (int)(rk + ck), g, cnt);
+            }
+        }
+    }
+    if (eval_count && lane == 0 && evals) atomicAdd(eval_count, evals);
+}
+
+// Buffers of the big-triangle list (grow-only, one entry per triangle at most).
+struct BandWork {
+    BandBig big{nullptr, nullptr, nullptr, nullptr};
+    size_t cap = 0;
+};
+
+int band_reserve(BandWork &bw, uint64_t ntri, Err &err)
+{
+    if (!bw.big.n) HIPCHK(hipMalloc((void **)&bw.big.n, 64));
+    if (bw.cap >= ntri && bw.big.tri) return 0;
+    (void)hipFree(bw.big.tri);
+    (void)hipFree(bw.big.chunks);
+    (void)hipFree(bw.big.pre);
+    bw.big.tri = bw.big.chunks = nullptr;
+    bw.big.pre = nullptr;
+    bw.cap = 0;
+    const size_t c = std::max<uint64_t>(ntri, 1);
+    HIPCHK(hipMalloc((void **)&bw.big.tri, c * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void **)&bw.big.chunks, c * sizeof(uint32_t)));
+    HIPCHK(hipMalloc((void **)&bw.big.pre, (c + 1) * sizeof(u64)));
+    bw.cap = c;
+    return 0;
+}
+
+void band_release(BandWork &bw)
+{
+    (void)hipFree(bw.big.tri);
+    (void)hipFree(bw.big.chunks);
+    (void)hipFree(bw.big.pre);
+    (void)hipFree(bw.big.n);
+    bw = BandWork{};
 }
 
 // One sweep cell update: the CPU's sequential check_neighbour chain (:90-102, :143-149)
@@ -537,6 +775,7 @@ struct Workspace {
     std::mutex mu;
     TileSweepWorkspace wf;
     SparseSweepWorkspace sp;
+    BandWork band;                      // the big-triangle list of the band phase
     float *out = nullptr;               // phi of the host-buffer entry point before its copy-out
     size_t cap_out = 0;
 };
@@ -602,6 +841,27 @@ inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap)
     return (unsigned)b;
 }
 
+// Waves of k_band_big: 8 per CU (its chunks are independent; an empty list exits at once).
+constexpr unsigned BAND_BIG_WG = 512;
+
+// The band phase of one call (or one Z-slab's planes [k_lo, k_hi)) on stream st.
+int band_enqueue(BandWork &bw, hipStream_t st, const float4 *soup, uint64_t ntri, const Grid &g, int band, float init,
+                 u64 *cell, uint32_t *cnt, unsigned long long *evals, int k_lo, int k_hi, Err &err)
+{
+    if (!ntri) return 0;
+    if (int rc = band_reserve(bw, ntri, err)) return rc;
+    HIPCHK(zero_async(bw.big.n, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(k_band_lds, dim3(grid_for((ntri + BAND_BT - 1) / BAND_BT, 1, 8192)), dim3(256), 0, st, soup, ntri,
+                       g, band, init, cell, cnt, evals, k_lo, k_hi, bw.big);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_band_big_scan, dim3(1), dim3(1024), 0, st, bw.big);
+    HIPCHK(hipGetLastError());
+    hipLaunchKernelGGL(k_band_big, dim3(BAND_BIG_WG), dim3(256), 0, st, soup, g, band, init, cell, cnt, evals, k_lo, k_hi,
+                       bw.big);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
 // Bounds-checked builds (make BOUNDS=1): report the first out-of-range index a kernel formed.
 int check_oob(Err &err, const char *where)
 {
@@ -651,11 +911,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     hipLaunchKernelGGL(k_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, ws->cell, ws->cnt, n, init_key);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev[1], st));
-    if (ntri) {
-        hipLaunchKernelGGL(k_band_lds, dim3(grid_for((ntri + BAND_BT - 1) / BAND_BT, 1, 8192)), dim3(256), 0, st, ws->soup, ntri, g, band,
-                           init, ws->cell, ws->cnt, ws->evals, 0, nk);
-        HIPCHK(hipGetLastError());
-    }
+    if ((rc = band_enqueue(ws->band, st, ws->soup, ntri, g, band, init, ws->cell, ws->cnt, ws->evals, 0, nk, err)))
+        return rc;
     HIPCHK(hipEventRecord(ev[2], st));
 
     // ---- sweeps ----
@@ -934,6 +1191,7 @@ struct SlabSession {
     size_t cap_soup = 0, cap_tri = 0, cap_xyz = 0, cap_out = 0;
     TileSweepWorkspace wf;
     SparseSweepWorkspace sp;
+    BandWork band;
     CommLayout cl;
     char *comm = nullptr;          // uncached, IPC-exported: inboxes, halo planes, inbound rings, flags
     char *peer[2] = {nullptr, nullptr};   // the lower / upper neighbour's comm (mapped)
@@ -955,6 +1213,7 @@ int slab_preload_kernels(Err &err)
 {
     if (getenv("SDFGEN_NO_KERNEL_PRELOAD")) return 0;   // diagnostics
     const void *k[] = {(const void *)k_prep_soup, (const void *)k_init, (const void *)k_band_lds,
+                       (const void *)k_band_big_scan, (const void *)k_band_big,
                        (const void *)k_sign, (const void *)k_sign_kfast, (const void *)k_sweep_tile<StCfgLat, true, false, false>,
                        (const void *)k_sweep_tile<StCfgLat, true, false, true>,
                        (const void *)k_sweep_tile<StCfgThr, true, false, false>,
@@ -1018,6 +1277,7 @@ void slab_free(SlabSession *S)
     (void)hipFree(S->comm);
     tile_sweep_release(S->wf);
     sparse_sweep_release(S->sp);
+    band_release(S->band);
     for (auto &e : S->ev)
         if (e) (void)hipEventDestroy(e);
     if (S->stream) (void)hipStreamDestroy(S->stream);
@@ -1086,6 +1346,7 @@ int slab_prepare(SlabSession *S, uint64_t ntri, Err &err)
         HIPCHK(hipMalloc((void **)&S->soup, 3 * std::max<uint64_t>(ntri, 1) * sizeof(float4)));
         S->cap_soup = 3 * std::max<uint64_t>(ntri, 1);
     }
+    if (int rc = band_reserve(S->band, ntri, err)) return rc;
     int ti = -1;
     for (int dk = -1; dk <= 1; dk += 2) {
         int cs, ce;
@@ -1160,11 +1421,9 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
                        S->cnt + plane_cells * S->k_begin, nslab, init_key);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev[1], st));
-    if (ntri) {
-        hipLaunchKernelGGL(k_band_lds, dim3(grid_for((ntri + BAND_BT - 1) / BAND_BT, 1, 8192)), dim3(256), 0, st, S->soup, ntri, g, band,
-                           init, S->cell, S->cnt, S->evals, S->k_begin, S->k_end);
-        HIPCHK(hipGetLastError());
-    }
+    if (int rc = band_enqueue(S->band, st, S->soup, ntri, g, band, init, S->cell, S->cnt, S->evals, S->k_begin, S->k_end,
+                              err))
+        return rc;
     HIPCHK(hipEventRecord(ev[2], st));
     tmark("band");
     S->launches = 0;
@@ -1543,6 +1802,75 @@ int sdfgen_hip_make_level_set3_device(int device, const uint32_t *d_tri, uint64_
                         err);
 }
 
+// Diagnostics: stage 1 only (prep, init, band + ray parity) on the current device, with the
+// pre-sweep state copied back: phi and closest_tri per cell (i-fastest) and the intersection
+// counts -- what oracle_band computes (cpu_lib/makelevelset3.cpp:196-236).  *big_n = big-triangle
+// entries the band phase handed to k_band_big.
+int sdfgen_hip_debug_band(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert, const float origin[3],
+                          float dx, int ni, int nj, int nk, int exact_band, float *phi, int32_t *ct, uint32_t *cnt,
+                          uint64_t *big_n, char *errbuf, size_t errlen)
+{
+    DeviceGuard dg_;
+    Err err{errbuf, errlen};
+    if (errbuf && errlen) errbuf[0] = 0;
+    int rc = validate(ntri, nvert, dx, ni, nj, nk, SDFGEN_LAYOUT_ARRAY3, err);
+    if (rc) return rc;
+    if (!phi || !ct || !cnt || !origin || (ntri && (!tri || !xyz))) return err.set(SDFGEN_HIP_EINVAL, "null pointer argument");
+    if (device_count_impl() <= 0) return err.set(SDFGEN_HIP_ENODEV, "no HIP GPU device is available");
+    int dev = 0;
+    HIPCHK(hipGetDevice(&dev));
+    Workspace *ws = nullptr;
+    if ((rc = get_ws(dev, &ws, err))) return rc;
+    std::lock_guard<std::mutex> lk(ws->mu);
+    HIPCHK(hipSetDevice(dev));
+    const uint64_t n = (uint64_t)ni * nj * nk;
+    if ((rc = grow(&ws->tri, &ws->cap_tri, std::max<uint64_t>(3 * ntri, 1), err))) return rc;
+    if ((rc = grow(&ws->xyz, &ws->cap_xyz, std::max<uint64_t>(3 * nvert, 1), err))) return rc;
+    if ((rc = grow(&ws->cell, &ws->cap_cell, n, err))) return rc;
+    if ((rc = grow(&ws->cnt, &ws->cap_cnt, n, err))) return rc;
+    if ((rc = grow(&ws->soup, &ws->cap_soup, 3 * std::max<uint64_t>(ntri, 1), err))) return rc;
+    if (!ws->err_flag) {
+        HIPCHK(hipMalloc((void **)&ws->err_flag, sizeof(int)));
+        HIPCHK(hipMalloc((void **)&ws->evals, sizeof(unsigned long long)));
+        HIPCHK(hipMalloc((void **)&ws->status, STATUS_N * sizeof(unsigned long long)));
+    }
+    hipStream_t st = ws->stream;
+    if (ntri) {
+        HIPCHK(hipMemcpyAsync(ws->tri, tri, 3 * ntri * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ws->xyz, xyz, 3 * nvert * sizeof(float), hipMemcpyHostToDevice, st));
+    }
+    Grid g{origin[0], origin[1], origin[2], dx, ni, nj, nk};
+    const float init = (float)(ni + nj + nk) * dx;
+    const u64 init_key = ((u64)__builtin_bit_cast(uint32_t, init) << 32) | 0xffffffffull;
+    HIPCHK(zero_async(ws->err_flag, sizeof(int), st));
+    if (ntri) {
+        hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, ws->tri, ntri, ws->xyz, nvert,
+                           ws->soup, ws->err_flag);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(k_init, dim3(grid_for(n, 256, 8192)), dim3(256), 0, st, ws->cell, ws->cnt, n, init_key);
+    HIPCHK(hipGetLastError());
+    if ((rc = band_enqueue(ws->band, st, ws->soup, ntri, g, exact_band, init, ws->cell, ws->cnt, nullptr, 0, nk, err)))
+        return rc;
+    int flag = 0;
+    uint32_t nb = 0;
+    HIPCHK(hipMemcpyAsync(&flag, ws->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    if (ntri) HIPCHK(hipMemcpyAsync(&nb, ws->band.big.n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(cnt, ws->cnt, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    std::vector<u64> cells(n);
+    HIPCHK(hipMemcpyAsync(cells.data(), ws->cell, n * sizeof(u64), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
+                             (unsigned long long)nvert);
+    for (uint64_t q = 0; q < n; ++q) {
+        const uint32_t hi = (uint32_t)(cells[q] >> 32);
+        memcpy(phi + q, &hi, 4);
+        ct[q] = lbl_of((uint32_t)cells[q]);
+    }
+    if (big_n) *big_n = nb;
+    return 0;
+}
+
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out)
 {
     if (!out) return SDFGEN_HIP_EINVAL;
@@ -1568,6 +1896,7 @@ int sdfgen_hip_release(void)
         hipFree(w->out);
         tile_sweep_release(w->wf);
         sparse_sweep_release(w->sp);
+        band_release(w->band);
         for (auto &e : w->ev) hipEventDestroy(e);
         hipStreamDestroy(w->stream);
         delete w;

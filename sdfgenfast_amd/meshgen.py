@@ -124,19 +124,60 @@ def grid_proportional(vertices: np.ndarray, target_nx: int, padding: int):
     return origin, dx, (target_nx, ny, nz)
 
 
-# Named workloads of BASELINE.json.
+def tetrahedron():
+    """A regular tetrahedron on alternate corners of the cube [-1, 1]^3: every face holds three
+    corners, so every face's bounding box -- and band box -- spans the whole grid (the coarse-mesh
+    extreme of the band phase: 4 triangles, 4 x the grid's cells of band work)."""
+    v = np.array([[-1, -1, -1], [1, 1, -1], [1, -1, 1], [-1, 1, 1]], np.float32)
+    t = np.array([[0, 2, 1], [0, 1, 3], [0, 3, 2], [1, 2, 3]], np.uint32)
+    return v, t
+
+
+def x3y4z5():
+    """The reference's benchmark mesh tests/resources/test_x3y4z5_bin.stl (36 triangles; stored as data
+    in tests/golden/resources), loaded with the native loader (bit-identical to the reference's
+    meshio::load_stl, tests/test_meshio_ref.py)."""
+    import os
+
+    from . import meshio
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                        "resources", "test_x3y4z5_bin.stl")
+    v, t = meshio.load_mesh(path)[:2]
+    return np.ascontiguousarray(v, np.float32), np.ascontiguousarray(t, np.uint32)
+
+
+# Named workloads: BASELINE.json's configs (SURVEY 8.d table), the reference's own published benchmark
+# (tests/benchmark_performance.cpp:151, 181-185: test_x3y4z5_bin.stl on proportional grids with padding
+# 2, README.md:256-260) and a coarse-mesh extreme for the band phase.
 WORKLOADS = {
     "c2_sphere70k_128": dict(nu=350, nv=101, n=128, padding=2),
     "c3_sphere1m_256": dict(nu=1000, nv=501, n=256, padding=2),
     "c4_sphere1m_512": dict(nu=1000, nv=501, n=512, padding=2),
     "c5_sphere4m_1024": dict(nu=2000, nv=1001, n=1024, padding=2),
+    "x3y4z5_prop64": dict(mesh="x3y4z5", n=64, padding=2, grid="proportional"),     # 64 x 84 x 104
+    "x3y4z5_prop128": dict(mesh="x3y4z5", n=128, padding=2, grid="proportional"),   # 128 x 169 x 211
+    "x3y4z5_prop256": dict(mesh="x3y4z5", n=256, padding=2, grid="proportional"),   # 256 x 340 x 424
+    "tetra_512": dict(mesh="tetrahedron", n=512, padding=2),
 }
 
 
-def workload(name: str):
-    """-> (vertices, triangles, origin, dx, (n, n, n)) for a named workload."""
+def workload_mesh(name: str):
     w = WORKLOADS[name]
-    v, t = bumpy_sphere(w["nu"], w["nv"])
+    m = w.get("mesh")
+    if m == "x3y4z5":
+        return x3y4z5()
+    if m == "tetrahedron":
+        return tetrahedron()
+    return bumpy_sphere(w["nu"], w["nv"])
+
+
+def workload(name: str):
+    """-> (vertices, triangles, origin, dx, (ni, nj, nk)) for a named workload."""
+    w = WORKLOADS[name]
+    v, t = workload_mesh(name)
     n = w["n"]
+    if w.get("grid") == "proportional":
+        origin, dx, dims = grid_proportional(v, n, w["padding"])
+        return v, t, origin, dx, dims
     origin, dx = grid_mode2b(v, n, n, n, w["padding"])
     return v, t, origin, dx, (n, n, n)

@@ -31,16 +31,24 @@ class GoldenCase:
         self.phi = z[f"{name}/phi"]  # sdf[i,j,k], C order (reference output)
 
 
-def load_golden():
-    z = np.load(os.path.join(GOLDEN, "cases.npz"))
+def load_golden(fname="cases.npz"):
+    z = np.load(os.path.join(GOLDEN, fname))
     return [GoldenCase(z, str(n)) for n in z["names"]]
 
 
 GOLDEN_CASES = load_golden()
+# far (> 2^31 cells), NaN and +-Inf vertices, wrapping exact_band values: the reference's own output
+# (tests/golden/make_golden.py --edge)
+EDGE_CASES = load_golden("edge_cases.npz")
 
 
 @pytest.fixture(params=GOLDEN_CASES, ids=[c.name for c in GOLDEN_CASES])
 def golden_case(request):
+    return request.param
+
+
+@pytest.fixture(params=EDGE_CASES, ids=[c.name for c in EDGE_CASES])
+def edge_case(request):
     return request.param
 
 

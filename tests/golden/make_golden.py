@@ -4,7 +4,9 @@ Run in the development container only (needs /root/reference):
 
     make -C oracle all ref
     python tests/golden/make_golden.py --small          # cases.npz (full phi arrays)
+    python tests/golden/make_golden.py --edge           # edge_cases.npz (far / NaN / Inf vertices, wrapping bands)
     python tests/golden/make_golden.py --large c2 c3 c4 # hashes.json (SHA-256 of phi)
+    python tests/golden/make_golden.py --large x3y4z5_prop64 tetra_512   # any meshgen.WORKLOADS name
 
 Every expected output comes from ``sdfgen::cpu::make_level_set3(..., num_threads=1)``
 (/root/reference/cpu_lib/makelevelset3.cpp:192, compiled by oracle/Makefile into
@@ -112,6 +114,85 @@ def run_small(out_path):
     print("wrote", out_path, os.path.getsize(out_path), "bytes")
 
 
+INT_MAX = 2**31 - 1
+
+
+def edge_cases():
+    """Inputs whose band boxes and ray lattices go through C++ int(double) out of range, NaN and
+    +-Inf, and the +band+1 wrap (cpu_lib/makelevelset3.cpp:206-212, 222-233; SURVEY App. A "Edge
+    semantics").  x86 cvttsd2si gives INT_MIN there; the boxes follow from clamp() after the wrap."""
+    cases = []
+    vc, tc = meshgen.unit_cube()
+    dims = (20, 22, 24)
+    o, dx = meshgen.grid_mode2b(vc, *dims, 2)
+    f32 = np.float32
+
+    def with_tris(extra_v, extra_t):
+        v = np.concatenate([vc, np.asarray(extra_v, np.float32)]).astype(np.float32)
+        t = np.concatenate([tc, np.asarray(extra_t, np.uint32) + len(vc)]).astype(np.uint32)
+        return v, t
+
+    base = np.array([[0.1, 0.05, 0.1], [0.3, 0.2, 0.15], [0.05, 0.3, 0.25]], np.float32)
+    # one vertex more than 2^31 cells from the grid, on each axis and sign (fi = +-3e9 and just past
+    # the int range)
+    for axis in range(3):
+        for sgn, mag in ((1, 3.0e9), (-1, 3.0e9), (1, 2.2e9), (-1, 2.16e9)):
+            far = base[2].copy()
+            far[axis] = f32(o[axis] + f32(sgn * mag) * f32(dx))
+            v, t = with_tris([base[0], base[1], far], [[0, 1, 2]])
+            cases.append((f"far_{'xyz'[axis]}{'+' if sgn > 0 else '-'}{int(mag / 1e7)}", v, t, o, dx, dims, 1))
+    # all three vertices far (the whole triangle off the grid, boxes from INT_MIN on every axis)
+    v, t = with_tris([[3e9 * dx, 1e10 * dx, -5e9 * dx], [-4e9 * dx, 2e9 * dx, 3.1e9 * dx], [1.0, 2.5e9 * dx, 0.2]],
+                     [[0, 1, 2]])
+    cases.append(("far_all", v, t, o, dx, dims, 1))
+    # NaN and +-Inf coordinates
+    for axis in range(3):
+        for name, val in (("nan", np.nan), ("pinf", np.inf), ("ninf", -np.inf)):
+            bad = base[2].copy()
+            bad[axis] = f32(val)
+            v, t = with_tris([base[0], base[1], bad], [[0, 1, 2]])
+            cases.append((f"{name}_{'xyz'[axis]}", v, t, o, dx, dims, 1))
+    v, t = with_tris([[np.nan, np.nan, np.nan], [np.inf, -np.inf, np.inf], [0.2, 0.2, 0.2]], [[0, 1, 2], [1, 2, 0]])
+    cases.append(("nan_inf_mixed", v, t, o, dx, dims, 1))
+    # exact_band large enough that int(max) + band + 1 wraps, very wide, zero and negative
+    for band in (INT_MAX, INT_MAX - 1, 2**30, 1000, 0, -1, -5, -(2**31) + 1):
+        cases.append((f"cube_band_{band}", vc, tc, o, dx, dims, band))
+    # far / non-finite vertices together with a band wide enough that every box is big
+    v, t = with_tris([base[0], base[1], [f32(o[0] - f32(3e9) * f32(dx)), 0.1, 0.1], [np.nan, 0.0, 0.0],
+                      [0.1, f32(o[1] + f32(2.5e9) * f32(dx)), 0.2]], [[0, 1, 2], [0, 1, 3], [4, 1, 0]])
+    cases.append(("far_nan_band40", v, t, o, dx, (48, 40, 44), 40))
+    vs, ts = meshgen.bumpy_sphere(40, 17)
+    os_, dxs = meshgen.grid_mode2b(vs, 36, 30, 40, 2)
+    v = np.concatenate([vs, [[np.nan, 0, 0], [0, np.inf, 0], [0, 0, f32(os_[2] + f32(2.3e9) * dxs)]]]).astype(np.float32)
+    t = np.concatenate([ts, [[len(vs), len(vs) + 1, len(vs) + 2], [0, 1, len(vs) + 2]]]).astype(np.uint32)
+    cases.append(("sphere_with_bad_tris", v, t, os_, dxs, (36, 30, 40), 2))
+    return cases
+
+
+def run_edge(out_path):
+    data = {}
+    names = []
+    with np.errstate(all="ignore"):
+        for name, v, t, o, dx, dims, band in edge_cases():
+            phi = O.ref_make_level_set3(v, t, o, dx, *dims, exact_band=band, num_threads=1)
+            mine = O.make_level_set3(v, t, o, dx, *dims, exact_band=band)
+            same = np.array_equal(phi.view(np.uint32), mine.view(np.uint32))
+            print(f"{name:24s} dims={dims} tris={t.shape[0]:5d} band={band} oracle==ref: {same}")
+            if not same:
+                raise SystemExit(f"oracle restatement differs from reference on {name}")
+            names.append(name)
+            data[f"{name}/vertices"] = v
+            data[f"{name}/triangles"] = t
+            data[f"{name}/origin"] = np.asarray(o, np.float32)
+            data[f"{name}/dx"] = np.float32(dx)
+            data[f"{name}/dims"] = np.asarray(dims, np.int32)
+            data[f"{name}/exact_band"] = np.int32(band)
+            data[f"{name}/phi"] = np.ascontiguousarray(phi)
+    data["names"] = np.array(names)
+    np.savez_compressed(out_path, **data)
+    print("wrote", out_path, os.path.getsize(out_path), "bytes")
+
+
 def digest(phi_f: np.ndarray) -> dict:
     """phi_f: (ni,nj,nk) array; hashes are over the i-fastest (Array3f) byte order."""
     flat = np.asfortranarray(phi_f).ravel(order="F").astype("<f4")
@@ -135,13 +216,13 @@ def run_large(keys, out_path):
         with open(out_path) as f:
             db = json.load(f)
     for key in keys:
-        name = LARGE[key]
+        name = LARGE.get(key, key)   # a short key or any meshgen.WORKLOADS name
         v, t, o, dx, dims = meshgen.workload(name)
         t0 = time.time()
         phi = O.ref_make_level_set3(v, t, o, dx, *dims, exact_band=1, num_threads=1)
         el = time.time() - t0
         rec = digest(phi)
-        rec.update({"dims": list(dims), "triangles": int(t.shape[0]), "vertices": int(v.shape[0]),
+        rec.update({"dims": [int(d) for d in dims], "triangles": int(t.shape[0]), "vertices": int(v.shape[0]),
                     "origin": [float(a) for a in o], "dx": float(dx),
                     "mesh_sha256": hashlib.sha256(v.tobytes() + t.tobytes()).hexdigest(),
                     "ref_seconds_1thread": round(el, 2)})
@@ -155,8 +236,11 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--small", action="store_true")
     ap.add_argument("--large", nargs="*", default=[])
+    ap.add_argument("--edge", action="store_true")
     a = ap.parse_args()
     if a.small:
         run_small(os.path.join(HERE, "cases.npz"))
+    if a.edge:
+        run_edge(os.path.join(HERE, "edge_cases.npz"))
     if a.large:
         run_large(a.large, os.path.join(HERE, "hashes.json"))

@@ -36,3 +36,13 @@ def test_cpu_backend_bad_index():
     t = np.array([[0, 1, 9]], np.uint32)
     with pytest.raises(IndexError):
         _lib.cpu_make_level_set3(v, t, (0, 0, 0), 0.1, 4, 4, 4, 1, 1)
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_cpu_backend_edge_semantics(edge_case, threads):
+    """Far (> 2^31 cells), NaN and infinite vertices and wrapping exact_band values: the reference's
+    own output (cpu_lib/makelevelset3.cpp:206-212, 222-233 on x86: int() -> INT_MIN, wrapping adds)."""
+    c = edge_case
+    with np.errstate(all="ignore"):
+        out = _lib.cpu_make_level_set3(c.vertices, c.triangles, c.origin, c.dx, *c.dims, c.exact_band, threads)
+    assert bits_equal(out, c.phi), diff_report(out, c.phi, c.dx)
