@@ -644,7 +644,6 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
     }
 }
 
-// Diagnostics kernels.
 // The sign pass with k-fastest output (SDFGEN_LAYOUT_KFAST: numpy (ni,nj,nk) C-order, the .sdf body):
 // k_sign's row walk along i would write every lane to its own line (stride nj*nk floats) -- 3.7 ms
 // at 512^3 against 0.4 for i-fastest.  Here a workgroup owns 64 rows (j, k0..k0+63) and walks i in
@@ -690,6 +689,7 @@ __global__ void __launch_bounds__(256) k_sign_kfast(const u64 *__restrict__ cell
     }
 }
 
+// Diagnostics kernels (the parity tests' geometry entry points).
 __global__ void k_debug_ptd(uint64_t n, const float *__restrict__ pts, float *__restrict__ out, int variant)
 {
     uint64_t q = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;

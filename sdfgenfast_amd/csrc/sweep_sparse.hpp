@@ -557,6 +557,15 @@ __device__ __forceinline__ void sp_push(const SpParams &P, int i, int j, int k, 
         __hip_atomic_store(P.push_up_halo + hp, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// In place (P.sv != null, S == X) this reads the upwind neighbours' labels through P.S with plain
+// loads while other lanes of the same launch store new labels into those cells: a neighbour may be
+// seen before or after its own change in this pass.  Both are allowed -- the pass only has to give
+// every cell whose upwind labels never change its final value; any cell that read a stale label has
+// an upwind neighbour that relabelled, and every relabel requests its 7 downstream cells
+// (sp_request_collect below) AFTER its store, so the repair pass re-evaluates them against the final
+// labels.  This relies on the 8-byte cell stores never tearing (one global_store_dwordx2 per cell)
+// and on S / X never being declared __restrict__ or read through the constant cache: the compiler must
+// not assume the stores leave S unchanged.
 template <bool SLAB = false>
 __device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32, unsigned *qmask, size_t (&tgt)[7])
 {

@@ -13,6 +13,10 @@
 #   prof=WORKLOAD    the same on another workload
 #   pmc              HBM + SQ counter passes on C3 (tools/pmc.sh, tools/pmc_sq.sh)
 #   py=SCRIPT,ARGS   python3 SCRIPT ARGS (a tools/ script)           -> gpurun_out/TAG_py<n>.log
+#                    (py=tools/fuzz_parity.py,200,3033  py=tools/c5_time.py  py=tools/wl_check.py,x3y4z5_prop256)
+#   nrank=N          bench.py --gpus N under torch.distributed.run with all N ranks on this box's ONE GPU:
+#                    a rehearsal of the Z-slab path (bit-exact check), not a scaling figure
+#                                                                    -> gpurun_out/TAG_nN_one_gpu_rehearsal.json.log
 # Every GPU step runs under its own time limit; a fault, abort or time-out (exit >= 124) ends the
 # session at once, a failing test (pytest exit 1) is reported and the session goes on.
 set -u
@@ -60,6 +64,10 @@ for s in "$@"; do
   pmc)
     run "${TAG}_pmc.log" 600 bash tools/pmc.sh c3_sphere1m_256
     run "${TAG}_pmc_sq.log" 600 bash tools/pmc_sq.sh c3_sphere1m_256 ;;
+  nrank=*)
+    N=${s#nrank=}
+    run "${TAG}_n${N}_one_gpu_rehearsal.json.log" 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" \
+      --master-addr 127.0.0.1 --master-port $((29541 + n)) bench.py --gpus "$N" --steps 2 --warmup 1 --no-cpu-baseline ;;
   py=*)
     a=${s#py=}
     run "${TAG}_py$n.log" 900 python3 ${a//,/ } ;;
