@@ -20,6 +20,8 @@ Side objects on the same line:
              C++/Python drop-in's path; SURVEY 8.d's definition of t), PCIe included.
   roofline   the first-pass tile sweep (the dominant kernel): HBM bytes vs 8 TB/s, plus `latency`:
              the launch's modelled critical path (steps) x the isolated per-step time.
+  ref_benchmark (N = 1) the reference's own published benchmark (test_x3y4z5_bin.stl on its 64/128/256
+             proportional grids): device-resident and host-array times, phases, parity, the published times.
   cpu_baseline  (N = 1) the reference's own cpu_lib on this host's cores (oracle/_ref, built from
              /root/reference) or, when that build is absent, the repository's deterministic native
              CPU backend -- both on the FULL C3 workload; `kind` says which.
@@ -254,6 +256,31 @@ def measure_host(workload, reps=3):
                     "value = steady state into a reused output array, first_call_ms = into a fresh one"}
 
 
+# The reference's own published benchmark (tests/benchmark_performance.cpp:151, 181-185; README.md:256-260):
+# test_x3y4z5_bin.stl (36 triangles) on proportional grids with padding 2, timed around one whole
+# make_level_set3 call with host arrays (std::chrono).  RTX 4090 (its CUDA backend, a different far-field
+# algorithm: SURVEY K2) and i9-13900K (cpu_lib, 1 / 20 threads) in ms.
+REF_PUBLISHED = {"x3y4z5_prop64": {"label": "64^3", "rtx4090_gpu_ms": 111, "cpu_1thread_ms": 738, "cpu_20thread_ms": 93},
+                 "x3y4z5_prop128": {"label": "128^3", "rtx4090_gpu_ms": 358, "cpu_1thread_ms": 5980, "cpu_20thread_ms": 748},
+                 "x3y4z5_prop256": {"label": "256^3", "rtx4090_gpu_ms": 1290, "cpu_1thread_ms": 48600, "cpu_20thread_ms": 4180}}
+
+
+def measure_ref_benchmark(dev, steps=5):
+    """The reference's published workload on this GPU: per grid the device-resident rate (inputs and phi
+    in HBM), the host-array call the reference times (PCIe included), the phase split and the parity
+    against the reference's own digest (tests/golden/hashes.json)."""
+    out = []
+    for name, pub in REF_PUBLISHED.items():
+        r = measure_single(name, steps, 1, dev, True)
+        h = measure_host(name)
+        out.append({"workload": name, "label": pub["label"], "dims": list(r["dims"]), "triangles": r["triangles"],
+                    "value": round(r["value"], 3), "unit": "Mvoxels/s", "ms_per_step": round(r["ms_per_step"], 4),
+                    "host_io_ms": h["ms_per_call"], "host_io_value": h["value"], "phases_ms": r["phases"],
+                    "parity": r["parity"], "published_ms": {k: v for k, v in pub.items() if k != "label"},
+                    "vs_rtx4090_host_io": round(pub["rtx4090_gpu_ms"] / h["ms_per_call"], 2)})
+    return out
+
+
 def step_latency(dev):
     """Isolated per-step time of the tile wavefront: a grid one tile wide (1024 x 9 x 9), so the
     first-pass launch is ONE tile per sweep in series -- no contention, pure step latency."""
@@ -402,6 +429,7 @@ def main():
             c4 = measure_single(args.c4_workload, 2, 1, dev, verify)
             res_side["zslab_c4"] = summary(c4, 1, "single-gpu", c4["ms_per_step"])
             res_side["host"] = measure_host(args.workload)
+            res_side["ref_benchmark"] = measure_ref_benchmark(dev)
     else:
         # single-GPU reference times for the efficiencies: rank 0 alone, the others wait
         t1 = [None, None]

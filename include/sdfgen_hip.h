@@ -141,7 +141,8 @@ typedef struct sdfgen_hip_profile {
     double slab_other_idle_ms;       /* the same for the other tasks */
     uint64_t slab_inbox_tasks, slab_other_tasks;
     int tile_cfg;                    /* first-pass tile kernel: 0 = 2 compute waves x 32 cells (latency-bound
-                                        grids), 1 = 1 compute wave x 64 cells (throughput-bound grids) */
+                                        grids), 1 = 1 compute wave x 64 cells (throughput-bound grids),
+                                        2 = 4 compute waves x 16 cells, four lanes per cell */
 } sdfgen_hip_profile;
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);

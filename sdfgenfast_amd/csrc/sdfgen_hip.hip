@@ -1096,7 +1096,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     p.sparse_sweeps = sparse_sweeps;
     p.tile_multi = multi_n;
     p.chain_steps = multi_n > 1 ? ws->wf.chain_steps : 0.0;
-    p.tile_cfg = multi_n > 1 && ws->wf.thr ? 1 : 0;
+    p.tile_cfg = multi_n > 1 ? ws->wf.cfg : 0;
     p.slabs = 1;
     p.sparse_first = sparse_sweeps ? sparse_first : 16;
 #ifdef SP_JACOBI_COUNT
@@ -1217,7 +1217,9 @@ int slab_preload_kernels(Err &err)
                        (const void *)k_sign, (const void *)k_sign_kfast, (const void *)k_sweep_tile<StCfgLat, true, false, false>,
                        (const void *)k_sweep_tile<StCfgLat, true, false, true>,
                        (const void *)k_sweep_tile<StCfgThr, true, false, false>,
-                       (const void *)k_sweep_tile<StCfgThr, true, false, true>, (const void *)k_sp_jacobi<true>,
+                       (const void *)k_sweep_tile<StCfgThr, true, false, true>,
+                       (const void *)k_sweep_tile<StCfgQuad, true, false, false>,
+                       (const void *)k_sweep_tile<StCfgQuad, true, false, true>, (const void *)k_sp_jacobi<true>,
                        (const void *)k_sp_jlist<true>, (const void *)k_sp_recheck<true>, (const void *)k_sp_slab_wait,
                        (const void *)k_sp_slab_halo, (const void *)k_sp_slab_export};
     for (const void *f : k) {
@@ -1602,7 +1604,7 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         p.sparse_claims = sp_ctl[SP_ENQ];
         p.tile_multi = S->tile_multi;
         p.chain_steps = S->tile_multi ? S->wf.chain_steps : 0.0;
-        p.tile_cfg = S->tile_multi && S->wf.thr ? 1 : 0;
+        p.tile_cfg = S->tile_multi ? S->wf.cfg : 0;
         p.slabs = S->nslabs;
         int khz = 0;   // device wall clock (wall_clock64) rate
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, S->device) != hipSuccess || khz <= 0)

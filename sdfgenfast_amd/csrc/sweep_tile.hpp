@@ -90,15 +90,16 @@ typedef int i4v __attribute__((ext_vector_type(4)));
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
 
-// Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, and the
-// waves per SIMD the register budget must allow.
-template <int NCW_, int RR_, bool TWIN_, int WPE_>
+// Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, the waves
+// per SIMD the register budget must allow, and quad lanes.
+template <int NCW_, int RR_, bool TWIN_, int WPE_, bool QUAD_ = false>
 struct StCfg {
     static constexpr int NCW = NCW_;                    // compute waves per tile
     static constexpr int CLW = ST_T / NCW;              // c-columns per compute wave
     static constexpr int CPW = ST_T * CLW;              // cells per compute wave
     static constexpr int RR = RR_;                      // neighbour ring slots
     static constexpr bool TWIN = TWIN_;                 // lane L + 32 is the twin of cell lane L
+    static constexpr bool QUAD = QUAD_;                 // four lanes per cell: lanes 4x .. 4x + 3 are cell x
     static constexpr int WPE = WPE_;
     static constexpr int LEAD = NCW > 1 ? RR - 4 : 0;   // max lead of wave w over wave w+1 (ring hazard)
     static constexpr int THREADS = 64 * (NCW + 1);      // compute waves + helper wave
@@ -106,8 +107,10 @@ struct StCfg {
     static constexpr int HALO0 = RING0 + RR * ST_NCOL;              // 17 streams x RH
     static constexpr int OWN0 = HALO0 + ST_NSTREAM * ST_RH;         // RO slots x 64 columns
     static constexpr int ENTS = OWN0 + ST_RO * ST_NCOL;
-    static_assert(NCW >= 1 && NCW <= 3 && ST_T % NCW == 0, "compute waves must split the tile's c-columns");
+    static_assert(NCW >= 1 && NCW <= 4 && ST_T % NCW == 0, "compute waves must split the tile's c-columns");
+    static_assert(NCW <= 3 || QUAD, "four compute waves: the quad-lane step only");
     static_assert(!TWIN || CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
+    static_assert(!QUAD || (CPW == 16 && !TWIN), "quad lanes: a compute wave owns 16 cells, 4 lanes each");
     // Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
     // neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the
     // lead between them (RR = 4 with 2 waves measured wrong results: no lead left).
@@ -122,14 +125,27 @@ using StCfgLat = StCfg<ST_NCW_DEF, ST_RR_DEF, (ST_TWIN != 0), ST_WPE_DEF>;
 #define ST_THR_WPE 2
 #endif
 using StCfgThr = StCfg<1, 4, false, ST_THR_WPE>;
+// Latency-bound grids, quad lanes: 4 compute waves of 16 cells, four lanes per cell -- every step
+// evaluates up to 4 candidates per cell in ONE pass (lane 4x + r takes the cell's r-th candidate in
+// check order) and the cell applies them in order from its quad (DPP broadcasts), so no step pays the
+// wave-wide compaction; ~48 KB LDS, 3 tiles per CU (5 waves each: 128 VGPRs).
+#ifndef ST_QUAD_WPE
+#define ST_QUAD_WPE 4
+#endif
+using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, true>;
 
+enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2 };
 // The configuration of a launch with `tiles` tasks per sweep: the throughput one once a sweep offers
-// well over the chip's resident 2-wave tiles (3 per CU).  SDFGEN_TILE_CFG=0/1 forces one (tests, A/B).
-inline bool st_use_thr(long long tiles)
+// well over the chip's resident tiles (3 per CU), the quad-lane one below (round 4: first pass 256^3
+// 13.73-13.89 -> 12.23-12.30 ms, 128^3 5.52-5.56 -> 4.78-4.79 ms against the twin-lane tiles; 512^3
+// 40.6 ms with the throughput tiles, 61.1 ms with quad lanes).  SDFGEN_TILE_CFG=0/1/2 forces one
+// (tests, A/B; 0 = the twin-lane tiles of round 3).
+inline int st_cfg(long long tiles)
 {
-    if (const char *e = getenv("SDFGEN_TILE_CFG")) return atoi(e) == 1;
-    return tiles > 2048;
+    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(2, atoi(e)));
+    return tiles > 2048 ? ST_CFG_THR : ST_CFG_QUAD;
 }
+inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
 
 constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
 
@@ -292,7 +308,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     __shared__ int s_pd[ST_NCW][14 * ST_CPW + 64];
     // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
     // compute wave w.
-    __shared__ __attribute__((aligned(16))) int s_hdr[4];
+    __shared__ __attribute__((aligned(16))) int s_hdr[ST_NCW < 4 ? 4 : 8];
     // halo entries < s_halo_ready[s] are in LDS; the extra last word is never "not ready"
     // (the stream index of lanes that read no halo stream)
     __shared__ int s_halo_ready[ST_NSTREAM + 1];
@@ -443,8 +459,12 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             // of cell lane L -- same cell, same candidate mask; L evaluates the cell's 1st, 3rd, ...
             // candidate and L + 32 its 2nd, 4th, ..., handed back with one v_permlane32_swap.
             const int w = wave;
-            const bool cell_lane = L < ST_CPW;
-            const int bl = L & (ST_T - 1), cl = ST_CLW * w + ((L >> 3) & (ST_CLW - 1));
+            // lane -> cell: cell lanes 0 .. CPW-1 (TWIN: lane L + 32 the twin of L); QUAD: cell x is lanes
+            // 4x .. 4x + 3, the lane's rank qr = L & 3, and lane 4x applies and stores
+            const int lcell = Cfg::QUAD ? (L >> 2) : L;
+            const int qr = Cfg::QUAD ? (L & 3) : 0;
+            const bool cell_lane = Cfg::QUAD ? (qr == 0) : (L < ST_CPW);
+            const int bl = lcell & (ST_T - 1), cl = ST_CLW * w + ((lcell >> 3) & (ST_CLW - 1));
             const int col_id = cl * ST_T + bl;
             const int b = b0 + bl, c = c0 + cl;
             const bool colx = b < P.B && c < P.ce;   // the cell (cell lane or twin)
@@ -452,6 +472,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             __builtin_amdgcn_s_setprio(ST_WORK_PRIO);
             // neighbour q's entry at step h: nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]) (ring slots are
             // ST_NCOL = 64 entries apart, halo slots 1)
+            // QUAD (128 VGPRs): ring and halo slots have the same mask (RR == RH), so the shift rides in
+            // the base's high bits and the three arrays are one (14 VGPRs fewer)
+            constexpr bool NB_PACK = Cfg::QUAD && ST_RR == ST_RH;
             int nb_base[7], nb_sh[7], nb_mask[7];
             {
                 static_assert(ST_NCOL == 64, "ring slot stride is a shift by 6");
@@ -459,6 +482,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     nb_base[q] = ST_RING0 + lcl * ST_T + lbl;
                     nb_sh[q] = 6;
                     nb_mask[q] = ST_RR - 1;
+                    if constexpr (NB_PACK) nb_base[q] |= 6 << 16;
                 };
                 auto halo = [&](int q, int s) {
                     nb_base[q] = ST_HALO0 + s * ST_RH;
@@ -488,7 +512,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #endif
                 const int a = h - bl - cl;
                 const bool act = col && a >= 0 && a < P.A;
-                const bool actx = (TWIN ? colx : col) && a >= 0 && a < P.A;   // the lanes that evaluate
+                const bool actx = ((TWIN || Cfg::QUAD) ? colx : col) && a >= 0 && a < P.A;   // the lanes that evaluate
                 // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
                 unsigned long long tw0 = 0;
                 for (;;) {
@@ -497,12 +521,20 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     // issued together.  (A volatile 16-byte read of s_hdr through a generic pointer
                     // compiled to a FLAT load: vector-memory latency on every poll, 8 % of the
                     // first pass at 256^3, 14 % at 512^3.)
-                    const i4v H = i4v{lds_ld(&s_hdr[0]), lds_ld(&s_hdr[1]), lds_ld(&s_hdr[2]), lds_ld(&s_hdr[3])};
+                    int hx, pm, pp;   // own entries ready, prog[w-1] (w > 0), prog[w+1] (w < NCW - 1)
+                    if constexpr (ST_NCW <= 3) {
+                        const i4v H = i4v{lds_ld(&s_hdr[0]), lds_ld(&s_hdr[1]), lds_ld(&s_hdr[2]), lds_ld(&s_hdr[3])};
+                        hx = H.x;
+                        pm = (w == 1) ? H.y : ((w == 2) ? H.z : H.w);
+                        pp = (w == 0) ? H.y : ((w == 1) ? H.z : H.w);
+                    } else {
+                        hx = lds_ld(&s_hdr[0]);
+                        pm = lds_ld(&s_hdr[w > 0 ? w : 1]);
+                        pp = lds_ld(&s_hdr[w < ST_NCW - 1 ? w + 2 : 1]);
+                    }
                     const int rA = lds_ld(&s_halo_ready[hsA]), rB = lds_ld(&s_halo_ready[hsB]),
                               rC = lds_ld(&s_halo_ready[hsC]);
-                    const bool own_ok = H.x > h;
-                    const int pm = (w == 1) ? H.y : ((w == 2) ? H.z : H.w);   // prog[w-1] (w > 0)
-                    const int pp = (w == 0) ? H.y : ((w == 1) ? H.z : H.w);   // prog[w+1]
+                    const bool own_ok = hx > h;
                     const bool ok = own_ok & ((w == 0) | (pm >= h)) & ((w == ST_NCW - 1) | (pp >= h - P.lead)) &
                                     (!act | (min(rA, min(rB, rC)) > a));
                     if (__all(ok)) break;
@@ -552,7 +584,10 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         const int aq = (q & 1) == 0 ? a - 1 : a;   // q = 0,2,4,6 read a-1
-                        ent[q] = nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]);
+                        if constexpr (NB_PACK)
+                            ent[q] = (nb_base[q] & 0xffff) + ((aq & (ST_RR - 1)) << (nb_base[q] >> 16));
+                        else
+                            ent[q] = nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]);
                         const uint32_t wq = __float_as_uint(s_ent[__umul24(ent[q], 3)].w);   // (full-rate 24-bit multiply)
                         lab[q] = lbl_of(wq);
                         lcq[q] = lc_of(wq);
@@ -584,7 +619,61 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 }
 #endif
                 bool twin_done = false;   // wave-uniform
-                if constexpr (TWIN) {
+                if constexpr (Cfg::QUAD) {
+                // ---- quad lanes: lane r of the cell's quad evaluates the cell's r-th candidate (and, in a
+                //      second pass only for cells with more than 4, its (r+4)-th); the cell lane takes the
+                //      quad's results by DPP broadcasts and applies them in the reference check order
+                //      (strict '<', first minimum wins: cpu_lib/makelevelset3.cpp:94-99, 143-149).  A rank
+                //      with no candidate reports NaN, which never passes '<' -- like a skipped check. ----
+                    twin_done = true;
+                    const f3 gx = st_gx(P, a, b, c);
+                    const unsigned f1 = fmask & (fmask - 1u), f2 = f1 & (f1 - 1u), f3 = f2 & (f2 - 1u);
+                    auto eval_rank = [&](unsigned fr, float &d, int &t, int &e) {
+                        const bool has = fr != 0u;
+                        const int qa = has ? __builtin_ctz(fr) : 0;
+                        int e1 = ent[0], t1 = lab[0];
+#pragma unroll
+                        for (int q = 1; q < 7; ++q) {   // static indices: no register-array indexing
+                            e1 = (qa == q) ? ent[q] : e1;
+                            t1 = (qa == q) ? lab[q] : t1;
+                        }
+                        e1 = has ? e1 : e_own;   // lanes without a candidate read a valid entry
+                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
+                        const float dd = ptd_wave(gx, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v3),
+                                                  v3.w);
+                        d = has ? dd : __builtin_nanf("");
+                        t = t1;
+                        e = e1;
+                        n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;
+                    };
+                    auto apply = [&](float d, int t, int e) {
+                        const bool take = d < phi;
+                        phi = take ? d : phi;
+                        ct = take ? t : ct;
+                        win = take ? e : win;
+                    };
+                    // lane k of each quad, broadcast (DPP quad_perm(k, k, k, k))
+#define ST_QB(x, k) __builtin_amdgcn_mov_dpp((x), (k) * 0x55, 0xf, 0xf, false)
+                    auto apply_quad = [&](float d, int t, int e, int nr) {
+                        const int di = __float_as_int(d);
+                        apply(__int_as_float(ST_QB(di, 0)), ST_QB(t, 0), ST_QB(e, 0));
+                        if (nr > 1) apply(__int_as_float(ST_QB(di, 1)), ST_QB(t, 1), ST_QB(e, 1));
+                        if (nr > 2) apply(__int_as_float(ST_QB(di, 2)), ST_QB(t, 2), ST_QB(e, 2));
+                        if (nr > 3) apply(__int_as_float(ST_QB(di, 3)), ST_QB(t, 3), ST_QB(e, 3));
+                    };
+                    if (__any(fmask != 0u)) {
+                        float d;
+                        int t, e;
+                        eval_rank(qr == 0 ? fmask : (qr == 1 ? f1 : (qr == 2 ? f2 : f3)), d, t, e);
+                        apply_quad(d, t, e, 4);
+                        if (__any(__popc(fmask) > 4u)) {   // ranks 4 .. 6 (at most 7 candidates)
+                            const unsigned f4 = f3 & (f3 - 1u), f5 = f4 & (f4 - 1u), f6 = f5 & (f5 - 1u);
+                            eval_rank(qr == 0 ? f4 : (qr == 1 ? f5 : (qr == 2 ? f6 : 0u)), d, t, e);
+                            apply_quad(d, t, e, 3);
+                        }
+                    }
+#undef ST_QB
+                } else if constexpr (TWIN) {
                 // ---- candidates in pairs: the cell lane takes the lowest remaining one, its twin
                 //      the next; one ptd per lane per pass, applied in the reference check order
                 //      (strict '<', first minimum wins: cpu_lib/makelevelset3.cpp:94-99, 143-149) ----
@@ -1058,7 +1147,7 @@ struct TileSweepWorkspace {
     size_t cap_mtasks = 0;
     long long mkey = -1;   // (ni, nj, nk, first sweep, count) of the uploaded graph
     double chain_steps = 0.0;   // modelled critical path of that graph, in steps
-    bool thr = false;           // the last multi-sweep launch ran the throughput configuration
+    int cfg = ST_CFG_LAT;       // the last multi-sweep launch's tile configuration (ST_CFG_*)
     unsigned mepoch = 0;
 };
 
@@ -1135,24 +1224,28 @@ inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int
     return 0;
 }
 
-// Launch k_sweep_tile with the configuration `thr` selects (st_use_thr), its lead cap applied.
-template <bool SLAB, bool TRACE, bool MULTI>
-inline void st_launch(bool thr, int grid, hipStream_t st, StParams &P, int lead_override)
+// Launch k_sweep_tile with the configuration `cfg` selects (st_cfg: ST_CFG_*), its lead cap applied.
+template <class Cfg, bool SLAB, bool TRACE, bool MULTI>
+inline void st_launch_cfg(const char *name, int grid, hipStream_t st, StParams &P, int lead_override)
 {
-    const int lead = thr ? StCfgThr::LEAD : StCfgLat::LEAD;
-    P.lead = (lead_override >= 0 && lead_override < lead) ? lead_override : lead;
+    P.lead = (lead_override >= 0 && lead_override < Cfg::LEAD) ? lead_override : Cfg::LEAD;
     if (getenv("SDFGEN_OCC")) {   // diagnostics: resident workgroups per CU
-        const void *f = thr ? (const void *)k_sweep_tile<StCfgThr, SLAB, TRACE, MULTI>
-                            : (const void *)k_sweep_tile<StCfgLat, SLAB, TRACE, MULTI>;
+        const void *f = (const void *)k_sweep_tile<Cfg, SLAB, TRACE, MULTI>;
         int occ = -1;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, thr ? StCfgThr::THREADS : StCfgLat::THREADS, 0);
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, f, Cfg::THREADS, 0);
         hipFuncAttributes fa;
         (void)hipFuncGetAttributes(&fa, f);
-        fprintf(stderr, "k_sweep_tile<%s>: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", thr ? "thr" : "lat", occ,
-                fa.numRegs, fa.sharedSizeBytes, fa.localSizeBytes);
+        fprintf(stderr, "k_sweep_tile<%s>: occupancy %d WG/CU, regs %d, lds %zu, local %zu\n", name, occ, fa.numRegs,
+                fa.sharedSizeBytes, fa.localSizeBytes);
     }
-    if (thr) hipLaunchKernelGGL((k_sweep_tile<StCfgThr, SLAB, TRACE, MULTI>), dim3(grid), dim3(StCfgThr::THREADS), 0, st, P);
-    else hipLaunchKernelGGL((k_sweep_tile<StCfgLat, SLAB, TRACE, MULTI>), dim3(grid), dim3(StCfgLat::THREADS), 0, st, P);
+    hipLaunchKernelGGL((k_sweep_tile<Cfg, SLAB, TRACE, MULTI>), dim3(grid), dim3(Cfg::THREADS), 0, st, P);
+}
+template <bool SLAB, bool TRACE, bool MULTI>
+inline void st_launch(int cfg, int grid, hipStream_t st, StParams &P, int lead_override)
+{
+    if (cfg == ST_CFG_THR) st_launch_cfg<StCfgThr, SLAB, TRACE, MULTI>("thr", grid, st, P, lead_override);
+    else if (cfg == ST_CFG_QUAD) st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
+    else st_launch_cfg<StCfgLat, SLAB, TRACE, MULTI>("lat", grid, st, P, lead_override);
 }
 
 // Enqueue one sweep direction on `st`.  Returns 0 or a negative SDFGEN_HIP_E* code.
@@ -1228,10 +1321,10 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
-    const bool thr = st_use_thr(ntasks);
-    if (slab.on) st_launch<true, false, false>(thr, grid, st, P, W.lead_override);
-    else if (P.trace) st_launch<false, true, false>(thr, grid, st, P, W.lead_override);
-    else st_launch<false, false, false>(thr, grid, st, P, W.lead_override);
+    const int cfg = st_cfg(ntasks);
+    if (slab.on) st_launch<true, false, false>(cfg, grid, st, P, W.lead_override);
+    else if (P.trace) st_launch<false, true, false>(cfg, grid, st, P, W.lead_override);
+    else st_launch<false, false, false>(cfg, grid, st, P, W.lead_override);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }
@@ -1528,13 +1621,13 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     // configuration by this slab's tiles per sweep (the largest sweep of the launch)
     int tiles = 0;
     for (int q = 0; q < ns; ++q) tiles = std::max(tiles, nJ * nKq[(size_t)q * nsl + me]);
-    W.thr = st_use_thr(tiles);
-    if (nsl > 1) st_launch<true, false, true>(W.thr, grid, st, P, W.lead_override);
+    W.cfg = st_cfg(tiles);
+    if (nsl > 1) st_launch<true, false, true>(W.cfg, grid, st, P, W.lead_override);
     else if (W.trace_multi) {   // diagnostics: per-task timeline of the whole launch (tools/trace_multi.py)
         if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(-5, "trace");
         P.trace = W.trace;
-        st_launch<false, true, true>(W.thr, grid, st, P, W.lead_override);
-    } else st_launch<false, false, true>(W.thr, grid, st, P, W.lead_override);
+        st_launch<false, true, true>(W.cfg, grid, st, P, W.lead_override);
+    } else st_launch<false, false, true>(W.cfg, grid, st, P, W.lead_override);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
 }

@@ -275,3 +275,16 @@ def test_gpu_host_entry_into_offset_and_pinned_arrays(layout):
         assert _hash_i_fastest(got) == db[name]["sha256_phi"], "pinned output"
     finally:
         rt.hipHostFree(p)
+
+
+def test_gpu_host_entry_fresh_outputs_c2_c4_c2():
+    """The shipped host path (sdfgen_hip_make_level_set3: pageable hipMemcpy in and out, no registration
+    of caller memory) into FRESH numpy arrays at C2 -> C4 -> C2 in one process, fresh inputs each time:
+    the sequence in which round 3's host-mapped prototype faulted (the C4 output is above
+    the ROCm runtime's own pinning threshold, the C2 ones below it).  Bit-exact against the reference."""
+    db = _hashes()
+    for name in ("c2_sphere70k_128", "c4_sphere1m_512", "c2_sphere70k_128"):
+        v, t, o, dx, dims = meshgen.workload(name)
+        got = _lib.make_level_set3(v.copy(), t.copy(), o, dx, *dims, 1, _lib.LAYOUT_ARRAY3)
+        assert _hash_i_fastest(got) == db[name]["sha256_phi"], name
+        del got, v, t

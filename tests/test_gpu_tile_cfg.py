@@ -1,5 +1,5 @@
-"""Both first-pass tile kernel configurations (sweep_tile.hpp StCfgLat / StCfgThr) against the
-oracle and the reference digests.  The library picks one by the tiles a sweep offers (st_use_thr:
+"""The first-pass tile kernel configurations (sweep_tile.hpp StCfgLat / StCfgThr / StCfgQuad) against
+the oracle and the reference digests.  The library picks one by the tiles a sweep offers (st_use_thr:
 256^3 runs the 2-wave tiles, 512^3 and 1024^3 the 1-wave tiles); SDFGEN_TILE_CFG forces either, so
 each is pinned on every grid shape here -- ragged, tiny, shifted, full size and Z-slabs."""
 import hashlib
@@ -16,10 +16,10 @@ from oracle import oracle as O
 from sdfgenfast_amd import _lib, meshgen
 
 pytestmark = pytest.mark.gpu
-CFGS = [0, 1]
+CFGS = [0, 1, 2]
 
 
-@pytest.fixture(params=CFGS, ids=["lat", "thr"])
+@pytest.fixture(params=CFGS, ids=["lat", "thr", "quad"])
 def cfg(request, monkeypatch):
     monkeypatch.setenv("SDFGEN_TILE_CFG", str(request.param))
     return request.param
@@ -69,9 +69,9 @@ def test_full_size_digest(cfg, name):
 
 
 def test_default_selection_by_grid(monkeypatch):
-    """No override: the 2-wave tiles at 256^3 (latency-bound), the 1-wave tiles at 512^3."""
+    """No override: the quad-lane tiles at 256^3 (latency-bound), the 1-wave tiles at 512^3."""
     monkeypatch.delenv("SDFGEN_TILE_CFG", raising=False)
-    for name, want in (("c3_sphere1m_256", 0), ("c4_sphere1m_512", 1)):
+    for name, want in (("c3_sphere1m_256", 2), ("c4_sphere1m_512", 1)):
         v, t, o, dx, dims = meshgen.workload(name)
         _lib.make_level_set3(v, t, o, dx, *dims, 1)
         assert _lib.last_profile()["tile_cfg"] == want, name
