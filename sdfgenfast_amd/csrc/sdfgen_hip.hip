@@ -959,7 +959,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     ws->wf.chi = n;
     ws->wf.ntri = ntri;
     ws->sp.ntri = ntri;
-    if (ws->wf.ctrl) HIPCHK(zero_async(ws->wf.ctrl + 1, sizeof(int), st));   // error bits of this call
+    if (ws->wf.ctrl) HIPCHK(zero_async(ws->wf.ctrl + 1, 15 * sizeof(int), st));   // error bits / report of this call
     if (sparse_first < 16 && ws->sp.ctl) HIPCHK(zero_async(ws->sp.ctl, SP_NCTL * sizeof(u64), st));
     // The first pass's tile sweeps as ONE launch whose sweeps overlap (tile_sweep_multi) unless
     // SDFGEN_TILE_MULTI=0, tracing is on, or the per-sweep halo buffers (17 GB at 1024^3) would
@@ -1121,7 +1121,10 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;
     }
-    if (wf_err) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
+    if (wf_err) {
+        st_watchdog_report(ws->wf, "make_level_set3");
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
+    }
     if (sp_ctl[SP_ERR] & 4ull) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sparse sweep: Jacobi list overflow");
     if (sp_ctl[SP_ERR]) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sparse sweep watchdog fired (work list stalled)");
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
@@ -1411,7 +1414,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     HIPCHK(zero_async(S->evals, sizeof(unsigned long long), st));
     HIPCHK(zero_async(S->tm, TM_N * sizeof(unsigned long long), st));
     S->wf.tm = S->tm;
-    if (S->wf.ctrl) HIPCHK(zero_async(S->wf.ctrl + 1, 3 * sizeof(int), st));
+    if (S->wf.ctrl) HIPCHK(zero_async(S->wf.ctrl + 1, 15 * sizeof(int), st));
     if (S->sp.ctl) HIPCHK(zero_async(S->sp.ctl, SP_NCTL * sizeof(u64), st));
     if (ntri) {
         hipLaunchKernelGGL(k_prep_soup, dim3(grid_for(ntri, 256, 8192)), dim3(256), 0, st, d_tri, ntri, d_xyz, nvert,

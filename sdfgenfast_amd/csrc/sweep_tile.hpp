@@ -136,14 +136,16 @@ using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, true>;
 
 enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2 };
 // The configuration of a launch with `tiles` tasks per sweep: the throughput one once a sweep offers
-// well over the chip's resident tiles (3 per CU), the quad-lane one below (round 4: first pass 256^3
-// 13.73-13.89 -> 12.23-12.30 ms, 128^3 5.52-5.56 -> 4.78-4.79 ms against the twin-lane tiles; 512^3
-// 40.6 ms with the throughput tiles, 61.1 ms with quad lanes).  SDFGEN_TILE_CFG=0/1/2 forces one
-// (tests, A/B; 0 = the twin-lane tiles of round 3).
+// more tiles than the chip holds at once (768: 3 per CU), the quad-lane one below (round 4, first
+// pass: 128^3 (256 tiles) 4.78 ms quad vs 5.52 twin lanes; 256^3 (1,024) 12.23-12.30 quad vs
+// 13.73-13.89 twin; 320^3 (1,600) 19.12-19.17 quad vs 18.39-18.45 throughput; 384^3 (2,304) 29.1-29.3
+// vs 23.6-23.9; 512^3 (4,096) 61.1 vs 40.6).  SDFGEN_TILE_CFG=0/1/2 forces one (tests, A/B; 0 = the
+// twin-lane tiles of round 3).
+constexpr long long ST_QUAD_MAX_TILES = 1200;
 inline int st_cfg(long long tiles)
 {
     if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(2, atoi(e)));
-    return tiles > 2048 ? ST_CFG_THR : ST_CFG_QUAD;
+    return tiles > ST_QUAD_MAX_TILES ? ST_CFG_THR : ST_CFG_QUAD;
 }
 inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
 
@@ -179,7 +181,7 @@ struct StParams {
     unsigned long long *hc;       // granules of tile-column edges: [nK][B][A]
     const int2 *tasks;            // (J,K) in dequeue order
     int *queue;                   // task counter (zeroed before each launch)
-    int *err;                     // bit 1: watchdog fired
+    int *err;                     // watchdog bits: 2 compute wave, 16 helper wave, 8 dependency wait, 4 inbox
     unsigned long long *stats;    // optional [evaluations, compute polls, helper idle polls, compute polls on own data]
     unsigned long long *trace;    // optional [task][start, end] wall_clock64 (100 MHz) of the compute wave
     float ox, oy, oz, dx;
@@ -231,6 +233,21 @@ __device__ __forceinline__ void st_fail(const StParams &P, int bit)
     atomicOr(P.err, bit);
     atomicMax(P.err + 1, P.sweep + 1);
     atomicCAS(P.err + 2, 0, (P.sweep + 1) | (bit << 8));   // the first failure: sweep + 1, its bit
+    atomicMax(P.queue, P.ntasks);
+}
+
+// The first failure of a launch also records where a compute wave gave up (ctrl[4..11], read by
+// st_watchdog_report): task, wave, step, own entries ready, prog[w-1], prog[w+1], the lane-min halo
+// readiness of the active lanes and their min a.
+__device__ __forceinline__ void st_fail_at(const StParams &P, int bit, int task, int w, int h, int hx, int pm, int pp,
+                                           int rmin, int amin)
+{
+    atomicOr(P.err, bit);
+    atomicMax(P.err + 1, P.sweep + 1);
+    if (atomicCAS(P.err + 2, 0, (P.sweep + 1) | (bit << 8)) == 0) {
+        const int v[8] = {task, w, h, hx, pm, pp, rmin, amin};
+        for (int q = 0; q < 8; ++q) __hip_atomic_store(P.err + 3 + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     atomicMax(P.queue, P.ntasks);
 }
 
@@ -548,7 +565,17 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     // step is issue-latency bound: -3 % first pass at 256^3)
                     __builtin_amdgcn_s_setprio(0);
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
-                        if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
+                        if (polls > ST_WATCHDOG) {   // this wave gave up (not an abort seen from elsewhere)
+                            const int rmin_ = act ? min(rA, min(rB, rC)) : 0x7fffffff, amin_ = act ? a : 0x7fffffff;
+                            int rm = rmin_, am = amin_;
+#pragma unroll
+                            for (int d_ = 32; d_ >= 1; d_ >>= 1) {
+                                rm = min(rm, __shfl_xor(rm, d_));
+                                am = min(am, __shfl_xor(am, d_));
+                            }
+                            if (L == 0) st_fail_at(P, 2, task, w, h, hx, pm, pp, rm, am);
+                        }
+                        if (L == 0) lds_st(&s_abort, 1);
                         h = nsteps;
                         break;
                     }
@@ -947,7 +974,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     if (!__any(go)) {
                         ++n_hpoll;
                         if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
-                            if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
+                            if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 16); }   // 16: a helper gave up
                             break;
                         }
                         const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
@@ -1082,7 +1109,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
                     ++n_hpoll;
                     if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
-                        if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 2); }
+                        if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 16); }
                         break;
                     }
                     const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
@@ -1149,6 +1176,9 @@ struct TileSweepWorkspace {
     double chain_steps = 0.0;   // modelled critical path of that graph, in steps
     int cfg = ST_CFG_LAT;       // the last multi-sweep launch's tile configuration (ST_CFG_*)
     unsigned mepoch = 0;
+    int last_ntasks = 0;        // tasks of the last multi-sweep launch (watchdog report) ...
+    int last_A = 0, last_B = 0, last_nJ = 0, last_ns = 0, last_nK[ST_MAXSW] = {0}, last_hbC[ST_MAXSW] = {0};
+    size_t last_nhb = 0, last_nhc = 0;
 };
 
 inline bool tile_sweep_supported(int ni, int nj, int nk) { return ni >= 2 && nj >= 2 && nk >= 2; }
@@ -1615,6 +1645,17 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
             }
         }
     }
+    W.last_ntasks = ntasks;
+    W.last_A = A;
+    W.last_B = B;
+    W.last_nJ = nJ;
+    W.last_ns = ns;
+    W.last_nhb = nhb;
+    W.last_nhc = nhc;
+    for (int q = 0; q < ns; ++q) {
+        W.last_nK[q] = P.sw[q].nK;
+        W.last_hbC[q] = P.sw[q].ce - P.sw[q].cs;
+    }
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
@@ -1630,6 +1671,79 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     } else st_launch<false, false, true>(W.cfg, grid, st, P, W.lead_override);
     if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
     return 0;
+}
+
+// After a fired watchdog (the stream has drained): where the last multi-sweep launch stopped -- the
+// task counter, the error words, per sweep the tasks whose completion flag is set, and the first
+// unfinished tasks with their dependencies.  Diagnostics, written to stderr.
+inline void st_watchdog_report(const TileSweepWorkspace &W, const char *who)
+{
+    int ctrl[12] = {0};
+    if (!W.ctrl || hipMemcpy(ctrl, W.ctrl, sizeof(ctrl), hipMemcpyDeviceToHost) != hipSuccess) return;
+    fprintf(stderr, "%s: tile watchdog: queue %d, error bits %d, max sweep+1 %d, first failure sweep+1 %d bit %d, "
+                    "cfg %d, epoch %u, call epoch %u\n", who, ctrl[0], ctrl[1], ctrl[2], ctrl[3] & 0xff, ctrl[3] >> 8, W.cfg,
+            W.epoch, W.mepoch);
+    if ((ctrl[3] >> 8) == 2)
+        fprintf(stderr, "  compute wave gave up: task %d wave %d step %d | own ready %d, prog[w-1] %d, prog[w+1] %d, "
+                        "halo ready (lane min) %d, a (lane min) %d\n", ctrl[4], ctrl[5], ctrl[6], ctrl[7], ctrl[8], ctrl[9],
+                ctrl[10], ctrl[11]);
+    const int n = W.last_ntasks;
+    if (n <= 0 || !W.mdone || !W.mtasks || !W.mdeps) return;
+    std::vector<unsigned> done(n);
+    std::vector<int4> tk(n);
+    std::vector<int> dep((size_t)n * ST_MAXDEP);
+    if (hipMemcpy(done.data(), W.mdone, n * sizeof(unsigned), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(tk.data(), W.mtasks, n * sizeof(int4), hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(dep.data(), W.mdeps, dep.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        return;
+    int per[ST_MAXSW] = {0}, tot[ST_MAXSW] = {0};
+    for (int t = 0; t < n; ++t) {
+        const int q = tk[t].z & (ST_MAXSW - 1);
+        ++tot[q];
+        per[q] += done[t] == W.mepoch;
+    }
+    for (int q = 0; q < ST_MAXSW; ++q)
+        if (tot[q]) fprintf(stderr, "  sweep slot %d: %d of %d tasks done\n", q, per[q], tot[q]);
+    int shown = 0;
+    for (int t = 0; t < n && shown < 8; ++t) {
+        if (done[t] == W.mepoch) continue;
+        fprintf(stderr, "  task %d (J %d, K %d, slot %d) not done; deps:", t, tk[t].x, tk[t].y, tk[t].z);
+        for (int m = 0; m < ST_MAXDEP; ++m) {
+            const int d = dep[(size_t)t * ST_MAXDEP + m];
+            if (d >= 0) fprintf(stderr, " %d%s", d, done[d] == W.mepoch ? "" : "*");
+        }
+        fprintf(stderr, "\n");
+        ++shown;
+    }
+    // the stuck compute wave's halo entries at a = amin: the granules the helper polls
+    const int task = ctrl[4], amin = ctrl[11];
+    if ((ctrl[3] >> 8) == 2 && task >= 0 && task < n && amin >= 0 && amin < W.last_A) {
+        const int J = tk[task].x, K = tk[task].y, q = tk[task].z;
+        const unsigned eq = W.epoch - (unsigned)(W.last_ns - 1 - q);   // slot q's epoch (one per sweep, in order)
+        const int A = W.last_A, B = W.last_B, hbC = W.last_hbC[q], nK = W.last_nK[q];
+        fprintf(stderr, "  task %d = tile (J %d, K %d) of slot %d (epoch %u), nJ %d nK %d, halo granules at a = %d:\n", task,
+                J, K, q, eq, W.last_nJ, nK, amin);
+        auto show = [&](const char *what, const unsigned long long *base, size_t idx) {
+            unsigned long long g = 0;
+            if (hipMemcpy(&g, base + idx, 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+            fprintf(stderr, "    %-30s epoch %u label %d%s\n", what, (unsigned)(g >> 32), lbl_of((uint32_t)g),
+                    (unsigned)(g >> 32) == eq ? " (ready)" : " (NOT ready)");
+        };
+        const unsigned long long *hb = W.mhb + (size_t)q * W.last_nhb, *hc = W.mhc + (size_t)q * W.last_nhc;
+        const int b0 = J * ST_T, c0 = K * ST_T;   // one GPU: cs = 0
+        char buf[64];
+        if (J > 0)
+            for (int L = 0; L < ST_T && c0 + L < hbC; ++L) {
+                snprintf(buf, sizeof(buf), "b-edge stream %d (c %d)", L, c0 + L);
+                show(buf, hb, ((size_t)(J - 1) * hbC + (c0 + L)) * A + amin);
+            }
+        if (K > 0)
+            for (int L = 0; L < ST_T && b0 + L < B; ++L) {
+                snprintf(buf, sizeof(buf), "c-edge stream %d (b %d)", ST_T + L, b0 + L);
+                show(buf, hc, ((size_t)(K - 1) * B + (b0 + L)) * A + amin);
+            }
+        if (J > 0 && K > 0) show("corner stream 16", hb, ((size_t)(J - 1) * hbC + (c0 - 1)) * A + amin);
+    }
 }
 
 inline void tile_sweep_release(TileSweepWorkspace &W)

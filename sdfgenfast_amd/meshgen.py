@@ -158,6 +158,9 @@ WORKLOADS = {
     "x3y4z5_prop128": dict(mesh="x3y4z5", n=128, padding=2, grid="proportional"),   # 128 x 169 x 211
     "x3y4z5_prop256": dict(mesh="x3y4z5", n=256, padding=2, grid="proportional"),   # 256 x 340 x 424
     "tetra_512": dict(mesh="tetrahedron", n=512, padding=2),
+    # tile-configuration crossover (diagnostics): 1,600 and 2,304 tiles per sweep
+    "sphere1m_320": dict(nu=1000, nv=501, n=320, padding=2),
+    "sphere1m_384": dict(nu=1000, nv=501, n=384, padding=2),
 }
 
 

@@ -79,6 +79,27 @@ __global__ void k_write8_agent_line(u64 *p, size_t nlines)
         __hip_atomic_store(p + 16 * i, (u64)i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// 16 passes over a 1 MiB buffer (L2-resident after the first): do agent-scope loads (sc1) refetch
+// every line from the memory side, like the first pass, or hit L2 like plain loads?
+__global__ void k_reread8_agent(const u64 *p, size_t n, int passes, u64 *sink)
+{
+    u64 acc = 0;
+    for (int r = 0; r < passes; ++r)
+        for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+            acc += __hip_atomic_load(p + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + r;
+    if (acc == 12345) sink[0] = acc;
+}
+__global__ void k_reread8(const u64 *p, size_t n, int passes, u64 *sink)
+{
+    u64 acc = 0;
+    for (int r = 0; r < passes; ++r) {
+        for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+            acc += p[i] + r;
+        asm volatile("" ::: "memory");   // every pass loads again
+    }
+    if (acc == 12345) sink[0] = acc;
+}
+
 int main()
 {
     const size_t bytes = 1ull << 30, lines = bytes / 128;
@@ -100,6 +121,9 @@ int main()
         hipLaunchKernelGGL(k_write8, g, b, 0, 0, (u64 *)buf, bytes / 8);
         hipLaunchKernelGGL(k_write8_agent, g, b, 0, 0, (u64 *)buf, bytes / 8);
         hipLaunchKernelGGL(k_write8_agent_line, g, b, 0, 0, (u64 *)buf, lines);
+        // 16 workgroups over one 1 MiB buffer: are the re-reads served by L2?
+        hipLaunchKernelGGL(k_reread8_agent, dim3(16), b, 0, 0, (const u64 *)buf, (size_t)(1u << 17), 16, (u64 *)sink);
+        hipLaunchKernelGGL(k_reread8, dim3(16), b, 0, 0, (const u64 *)buf, (size_t)(1u << 17), 16, (u64 *)sink);
         CHK(hipGetLastError());
         CHK(hipDeviceSynchronize());
     }

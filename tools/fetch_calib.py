@@ -21,7 +21,10 @@ KNOWN = {"k_read16": ("16-B coalesced plain loads", GIB, LINES),
          "k_gather16_line": ("one 16-B plain load per 128-B line, scattered", 16 * LINES, LINES),
          "k_write8": ("8-B coalesced plain stores", GIB, LINES),
          "k_write8_agent": ("8-B coalesced agent-scope atomic stores", GIB, LINES),
-         "k_write8_agent_line": ("one 8-B agent-scope store per 128-B line", 8 * LINES, LINES)}
+         "k_write8_agent_line": ("one 8-B agent-scope store per 128-B line", 8 * LINES, LINES),
+         # 16 passes over 1 MiB (8,192 lines): FETCH/line ~64 B = one fetch per line, ~16 x 64 B = every pass
+         "k_reread8_agent": ("16 passes of 8-B agent-scope loads over 1 MiB", 16 << 20, 8192),
+         "k_reread8": ("16 passes of 8-B plain loads over 1 MiB", 16 << 20, 8192)}
 
 
 def run(counter):

@@ -59,7 +59,7 @@ for s in "$@"; do
     [[ $s == prof=* ]] && w=${s#prof=}
     rm -rf "gpurun_out/${TAG}_prof_$w"
     run "${TAG}_prof_$w.log" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/${TAG}_prof_$w" -o run -- \
-      python3 bench.py --workload "$w" --steps 5 --warmup 1 --no-cpu-baseline --no-side
+      python3 bench.py --workload "$w" --steps 5 --warmup 1 --no-cpu-baseline --no-side --no-latency
     find "gpurun_out/${TAG}_prof_$w" -name "*kernel_stats*" ;;
   pmc)
     run "${TAG}_pmc.log" 600 bash tools/pmc.sh c3_sphere1m_256

@@ -24,22 +24,26 @@ uncached system-scope round trip is 0.82 us, tools/uc_lat).
 """
 import json
 
-# ---- measured inputs (one MI355X, round 3) ----
+# ---- measured inputs (one MI355X, round 4) ----
 INPUTS = {
-    "c3_sphere1m_256": {   # bench r03h: 17.82 ms total; tile launch 13.85 ms; 8 sparse sweeps 3.05 ms
-        "dims": (256, 256, 256), "t_local": 0.8492, "t_first": 13.846, "t_second": 3.0499,
-        "t_repair_per_sweep": 0.244,   # k_sp_recheck per sweep at C3 (r03g kernel trace, mean of 8)
-        "t_first_work": 5.6,           # tile work at full throughput: C4's first pass x 1/8 of the cells
+    "c3_sphere1m_256": {   # bench r04f: 16.13 ms total; quad-lane tile launch 12.13 ms; 8 sparse sweeps 3.03 ms
+        "dims": (256, 256, 256), "t_local": 0.8651, "t_first": 12.128, "t_second": 3.0268,
+        "t_repair_per_sweep": 0.247,   # k_sp_recheck per sweep at C3 (r04f kernel trace, mean of 8 x 6 calls)
+        "t_first_work": 5.2,           # tile work at full throughput: C4's first pass x 1/8 of the cells
+        "longest_chain": 86,           # longest relabel chain of a second-pass sweep (oracle)
     },
-    "c4_sphere1m_512": {   # bench r03h zslab_c4 side object: 59.79 ms; tile 44.86 ms; sparse 12.78 ms
-        "dims": (512, 512, 512), "t_local": 1.9689, "t_first": 44.862, "t_second": 12.7841,
+    "c4_sphere1m_512": {   # bench r04f zslab_c4 side object: 55.63 ms; tile 41.39 ms; sparse 12.17 ms
+        "dims": (512, 512, 512), "t_local": 1.9576, "t_first": 41.394, "t_second": 12.171,
         "t_repair_per_sweep": 0.62,    # repair_ms per sweep, 2-slab rehearsal (r03c_n2 zslab_c4), median
-        "t_first_work": 44.862,        # throughput-bound at one GPU: the launch itself
+        "t_first_work": 41.394,        # throughput-bound at one GPU: the launch itself
+        "longest_chain": 172,          # not measured at C4: 2 x C3's (chains scale with the grid edge)
     },
 }
-S_ISO_US = 1.559     # isolated tile step (bench latency probe, 1024x9x9 grid)
+S_ISO_US = 1.3164    # isolated tile step, quad-lane tiles (bench r04f latency probe, 1024x9x9 grid)
 H_X_US = 2.0         # cross-GPU granule hand-off over xGMI (assumed; on-chip uncached round trip 0.82 us)
 H_FLAG_US = 2.0      # one DONE / READY flag hand-off between neighbour GPUs (assumed, as h_x)
+LINK_IDLE_US = 1.25  # one repair chain link on an idle chip: ~4 returning atomics + 2 dependent loads, ~3,000 cycles
+                     # (round 3, tools/xcd_lat); under the 1-GPU repair's own load it is ~4.7 us
 ST_T = 8
 DIRS = [(+1, +1, +1), (-1, -1, -1), (+1, +1, -1), (-1, -1, +1), (+1, -1, +1), (-1, +1, -1), (+1, -1, -1), (-1, +1, +1)]
 
@@ -116,15 +120,23 @@ def predict(name, inp, ns=(1, 2, 4, 8)):
         chain = cn * S_ISO_US * 1e-3 + 8 * (n - 1) * H_X_US * 1e-3
         work = inp["t_first_work"] / n
         first = max(chain, work) * (1.0 + (crowd - 1.0) / n)
-        second = 8 * (t_scan / n + inp["t_repair_per_sweep"] + (2 * H_FLAG_US + (n - 1) * H_X_US) * 1e-3 * (n > 1))
+        # repair term: measured at one GPU (upper: it does not shrink with N) and the longest chain at the
+        # idle-chip link latency (lower: a slab of 1/N of the cells runs 1/N of the concurrent chains)
+        rep_hi = inp["t_repair_per_sweep"]
+        rep_lo = min(rep_hi, inp["longest_chain"] * LINK_IDLE_US * 1e-3) if n > 1 else rep_hi
+        hand = (2 * H_FLAG_US + (n - 1) * H_X_US) * 1e-3 * (n > 1)
+        second = 8 * (t_scan / n + rep_hi + hand)
+        second_lo = 8 * (t_scan / n + rep_lo + hand)
         local = inp["t_local"] / n
         total = local + first + second
         rows.append({"n": n, "chain_steps": round(cn, 1), "first_chain_ms": round(chain, 3),
                      "first_work_ms": round(work, 3), "first_ms": round(first, 3), "second_ms": round(second, 3),
-                     "local_ms": round(local, 3), "total_ms": round(total, 3)})
+                     "second_ms_if_links_idle": round(second_lo, 3), "local_ms": round(local, 3),
+                     "total_ms": round(total, 3), "total_ms_if_links_idle": round(local + first + second_lo, 3)})
     t1 = rows[0]["total_ms"]
     for r in rows:
         r["efficiency"] = round(t1 / (r["n"] * r["total_ms"]), 3)
+        r["efficiency_if_links_idle"] = round(t1 / (r["n"] * r["total_ms_if_links_idle"]), 3)
     return {"workload": name, "crowd_factor_1gpu": round(crowd, 3), "inputs": inp, "s_iso_us": S_ISO_US,
             "h_x_us": H_X_US, "rows": rows}
 
