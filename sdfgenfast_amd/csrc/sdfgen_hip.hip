@@ -1121,6 +1121,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;
     }
+    if (wf_err & 64) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep: a task-table row failed its check (table memory corrupted)");
     if (wf_err) {
         st_watchdog_report(ws->wf, "make_level_set3");
         return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
@@ -1197,8 +1198,7 @@ struct SlabSession {
     BandWork band;
     CommLayout cl;
     char *comm = nullptr;          // uncached, IPC-exported: inboxes, halo planes, inbound rings, flags
-    char *peer[2] = {nullptr, nullptr};   // the lower / upper neighbour's comm (mapped)
-    bool peer_ipc[2] = {false, false};
+    char *peer[2] = {nullptr, nullptr};   // the lower / upper neighbour's comm (mapped, comm_import)
     unsigned long long sync_epoch = 0;    // neighbour handshakes issued (same count on every slab)
     uint64_t prepared_ntri = ~0ull;       // slab_prepare was run for this many triangles
     int sparse_sweeps = 0, tile_multi = 0;
@@ -1206,6 +1206,90 @@ struct SlabSession {
     int launches = 0;
     std::mutex mu;
 };
+
+// Uncached blocks are never returned to the runtime while the process runs.  After hipFree of
+// an uncached (MTYPE UC) block, a later plain hipMalloc that is handed the same virtual range has
+// been seen to lose stores and read zeros on the GPU: the first one-GPU call after an in-process
+// two-slab call placed its halo buffer exactly on a freed comm block and failed (digest mismatch
+// or a tile hand-off never arriving, 3 of 3 runs), and never failed when the block was kept
+// ("freed uncached memory").  So freed sessions hand their block back to this
+// per-process pool, the next session on the device takes the smallest free block that fits, and
+// the pool (a few 2 MiB blocks per grid plane size) lives until the process exits.  The IPC
+// handle of a block is exported once; peers map each handle once (comm_import) and keep it, for
+// the same reason on the importing side.
+struct CommBlock {
+    int device;
+    char *p;
+    size_t bytes;
+    bool busy;
+    bool exported;
+    hipIpcMemHandle_t handle;
+};
+std::mutex g_comm_mu;
+std::vector<CommBlock> g_comm;
+
+int comm_acquire(int device, size_t bytes, char **out, Err &err)
+{
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    CommBlock *best = nullptr;
+    for (CommBlock &b : g_comm)
+        if (!b.busy && b.device == device && b.bytes >= bytes && (!best || b.bytes < best->bytes)) best = &b;
+    if (!best) {
+        CommBlock b{};
+        b.device = device;
+        b.bytes = bytes;
+        HIPCHK(hipExtMallocWithFlags((void **)&b.p, bytes, hipDeviceMallocUncached));
+        g_comm.push_back(b);
+        best = &g_comm.back();
+    }
+    best->busy = true;
+    *out = best->p;
+    return 0;
+}
+
+void comm_return(char *p)
+{
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    for (CommBlock &b : g_comm)
+        if (b.p == p) b.busy = false;
+}
+
+int comm_export(char *p, hipIpcMemHandle_t *h, Err &err)
+{
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    for (CommBlock &b : g_comm)
+        if (b.p == p) {
+            if (!b.exported) {
+                HIPCHK(hipIpcGetMemHandle(&b.handle, p));
+                b.exported = true;
+            }
+            *h = b.handle;
+            return 0;
+        }
+    return err.set(SDFGEN_HIP_ERUNTIME, "slab communication block not found");
+}
+
+struct CommImport {
+    int device;
+    hipIpcMemHandle_t handle;
+    void *p;
+};
+std::vector<CommImport> g_comm_imports;
+
+int comm_import(int device, const hipIpcMemHandle_t &h, void **out, Err &err)
+{
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    for (const CommImport &m : g_comm_imports)
+        if (m.device == device && memcmp(&m.handle, &h, sizeof(h)) == 0) {
+            *out = m.p;
+            return 0;
+        }
+    void *p = nullptr;
+    HIPCHK(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    g_comm_imports.push_back(CommImport{device, h, p});
+    *out = p;
+    return 0;
+}
 
 // Resolve every kernel a slab launches before any of its work is enqueued.  A kernel's first
 // launch makes the HIP runtime load it (deferred code-object loading); doing that while this
@@ -1255,7 +1339,10 @@ int slab_alloc(SlabSession *S, Err &err)
     // no cache, so every system-scope load of a poll reads what the remote system-scope store
     // wrote, mid-kernel.  Whole 2 MiB: a dedicated allocation that IPC maps as is.
     S->cl.init(plane);
-    HIPCHK(hipExtMallocWithFlags((void **)&S->comm, S->cl.bytes, hipDeviceMallocUncached));
+    if (int rc = comm_acquire(S->device, S->cl.bytes, &S->comm, err)) return rc;
+    if (getenv("SDFGEN_DEBUG_VA"))
+        fprintf(stderr, "VA slab %d comm [%p, %p) uncached; cell %p\n", S->slab, (void *)S->comm,
+                (void *)(S->comm + S->cl.bytes), (void *)S->cell_mem);
     HIPCHK(hipMemset(S->comm, 0, S->cl.bytes));   // epoch 0 is never published, flags start at 0
     HIPCHK(hipDeviceSynchronize());
     return 0;
@@ -1266,8 +1353,9 @@ void slab_free(SlabSession *S)
     if (S->device < 0) return;
     (void)hipSetDevice(S->device);
     if (S->stream) (void)hipStreamSynchronize(S->stream);
-    for (int side = 0; side < 2; ++side)
-        if (S->peer_ipc[side] && S->peer[side]) (void)hipIpcCloseMemHandle(S->peer[side]);
+    // the neighbours' blocks stay mapped (comm_import) and this slab's block goes back to the pool
+    if (S->comm) comm_return(S->comm);
+    S->comm = nullptr;
     (void)hipFree(S->cell_mem);
     (void)hipFree(S->alt_mem);
     (void)hipFree(S->cnt_mem);
@@ -1279,7 +1367,6 @@ void slab_free(SlabSession *S)
     (void)hipFree(S->evals);
     (void)hipFree(S->arrive);
     (void)hipFree(S->tm);
-    (void)hipFree(S->comm);
     tile_sweep_release(S->wf);
     sparse_sweep_release(S->sp);
     band_release(S->band);
@@ -1570,7 +1657,7 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
     unsigned long long evals = 0, sp_ctl[4] = {0, 0, 0, 0}, tm[TM_N];
     HIPCHK(hipMemcpyAsync(&flag, S->err_flag, sizeof(int), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(tm, S->tm, sizeof(tm), hipMemcpyDeviceToHost, st));
-    if (S->wf.ctrl) HIPCHK(hipMemcpyAsync(wf_err, S->wf.ctrl + 1, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
+    if (S->wf.ctrl) HIPCHK(hipMemcpyAsync(wf_err, S->wf.ctrl + 1, sizeof(wf_err), hipMemcpyDeviceToHost, st));
     if (S->sparse_sweeps && S->sp.ctl) HIPCHK(hipMemcpyAsync(sp_ctl, S->sp.ctl, sizeof(sp_ctl), hipMemcpyDeviceToHost, st));
     HIPCHK(hipMemcpyAsync(&evals, S->evals, sizeof(evals), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -1626,6 +1713,8 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         p.slab_other_tasks = tm[TM_OTHER_TASKS];
         *prof = p;
     }
+    if (wf_err[0] & 64)
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: a task-table row failed its check (table memory corrupted)", S->slab);
     if (wf_err[0] & 4)
         return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: upstream slab's plane never arrived (sweep %d)", S->slab,
                        wf_err[1] - 1);
@@ -2018,7 +2107,7 @@ int sdfgen_hip_slab_export(sdfgen_hip_slab *h, void *handle, char *errbuf, size_
     static_assert(sizeof(hipIpcMemHandle_t) <= SDFGEN_HIP_IPC_HANDLE_BYTES, "IPC handle size");
     HIPCHK(hipSetDevice(h->s.device));
     hipIpcMemHandle_t m;
-    HIPCHK(hipIpcGetMemHandle(&m, h->s.comm));
+    if (int rc = comm_export(h->s.comm, &m, err)) return rc;
     memset(handle, 0, SDFGEN_HIP_IPC_HANDLE_BYTES);
     memcpy(handle, &m, sizeof(m));
     return 0;
@@ -2040,9 +2129,8 @@ int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *h, const void *lower, const voi
         hipIpcMemHandle_t m;
         memcpy(&m, hs[side], sizeof(m));
         void *p = nullptr;
-        HIPCHK(hipIpcOpenMemHandle(&p, m, hipIpcMemLazyEnablePeerAccess));
+        if (int rc = comm_import(S->device, m, &p, err)) return rc;
         S->peer[side] = (char *)p;
-        S->peer_ipc[side] = true;
         // the mapping must cover the neighbour's whole block (same grid => same layout)
         void *base = nullptr;
         size_t size = 0;

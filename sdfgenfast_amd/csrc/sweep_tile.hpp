@@ -208,9 +208,34 @@ struct StParams {
     const int *deps;              // [task][ST_MAXDEP]: earlier tasks (previous sweep) to wait for, -1 = none
     unsigned *done;               // [task] = call_epoch once the task's cell stores are visible
     unsigned call_epoch;
+    unsigned table_gen;           // upload count of the tables: part of every row's stamp
     StSweep sw[ST_MAXSW];
     unsigned long long *tm;       // Z-slab phase timers (sweep_sparse.hpp TM_*; null: not recorded)
 };
+
+// Stamp of one row of the multi-sweep task tables (tile_sweep_multi writes it into mtasks[].w):
+// the row's position, its (J, K, slot), a weighted sum of its dependency list and the upload count,
+// so a row left over from an earlier upload does not pass for the current one.
+__host__ __device__ inline unsigned st_task_check(int task, int J, int K, int q, unsigned gen, unsigned dsum)
+{
+    unsigned h = gen * 0x9E3779B1u ^ (unsigned)task * 0x85EBCA77u;
+    h ^= ((unsigned)J << 20) ^ ((unsigned)K << 8) ^ (unsigned)q;
+    h ^= dsum * 0xC2B2AE3Du;
+    h ^= h >> 15;
+    h *= 0x2C1B3C6Du;
+    return h ^ (h >> 13);
+}
+__host__ __device__ inline unsigned st_dep_term(int m, int dep) { return (unsigned)(dep + 1) * (unsigned)(2 * m + 1); }
+
+// Wave-uniform: does this row (tk read by every lane, dep = lane L's dependency) carry its stamp?
+__device__ __forceinline__ bool st_task_row_ok(const StParams &P0, int task, int4 tk, int dep, int L)
+{
+    unsigned d = L < ST_MAXDEP ? st_dep_term(L, dep) : 0u;
+#pragma unroll
+    for (int o = ST_MAXDEP / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+    d = __shfl(d, 0, 64);
+    return __all((unsigned)tk.w == st_task_check(task, tk.x, tk.y, tk.z, P0.table_gen, d));
+}
 
 __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
 {
@@ -331,6 +356,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     __shared__ int s_halo_ready[ST_NSTREAM + 1];
     __shared__ int s_abort;
     __shared__ int s_task;
+    __shared__ int4 s_tk;
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -359,7 +385,28 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         const unsigned long long t_claim = (TRACE && MULTI && P.trace) ? wall_clock64() : 0ull;
         int J, K;
         if (MULTI) {
-            const int4 tk = P0.mtasks[task];
+            // wave 0 reads the task's row of both tables and checks it against the upload's
+            // stamp (st_task_check); the other waves take (J, K, slot) from LDS.  (Added while
+            // chasing the freed-uncached-memory failure, DESIGN.md §6: the rows were never wrong
+            // there, but a corrupted table would otherwise run wrong tiles silently.)
+            int dep = -1;
+            if (wave == 0) {
+                int4 tk = P0.mtasks[task];
+                dep = L < ST_MAXDEP ? P0.deps[(size_t)task * ST_MAXDEP + L] : -1;
+                if (!st_task_row_ok(P0, task, tk, dep, L)) {
+                    // not the row this launch's upload wrote (the table memory was overwritten or
+                    // read stale): fail loudly rather than run a wrong tile
+                    if (L == 0) {
+                        atomicAdd(P.err + 11, 1);
+                        st_fail(P, 64);
+                    }
+                    tk = make_int4(0, 0, 0, 0);
+                    dep = -1;
+                }
+                if (L == 0) s_tk = tk;
+            }
+            __syncthreads();
+            const int4 tk = s_tk;
             J = tk.x;
             K = tk.y;
             const StSweep &sw = P0.sw[tk.z];
@@ -382,7 +429,6 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             }
             if (wave == 0) {
                 // the previous sweep's tiles under and around this one: their cell stores first
-                const int dep = L < ST_MAXDEP ? P0.deps[(size_t)task * ST_MAXDEP + L] : -1;
                 bool ok = dep < 0;
                 for (unsigned spins = 0;; ++spins) {
                     if (!ok) ok = __hip_atomic_load(P0.done + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -1176,6 +1222,7 @@ struct TileSweepWorkspace {
     double chain_steps = 0.0;   // modelled critical path of that graph, in steps
     int cfg = ST_CFG_LAT;       // the last multi-sweep launch's tile configuration (ST_CFG_*)
     unsigned mepoch = 0;
+    unsigned mgen = 0;     // uploads of the multi-sweep tables (st_task_check)
     int last_ntasks = 0;        // tasks of the last multi-sweep launch (watchdog report) ...
     int last_A = 0, last_B = 0, last_nJ = 0, last_ns = 0, last_nK[ST_MAXSW] = {0}, last_hbC[ST_MAXSW] = {0};
     size_t last_nhb = 0, last_nhc = 0;
@@ -1545,14 +1592,17 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
             while (g >= base[(size_t)(q + 1) * nsl]) ++q;
             const size_t x = (size_t)q * nsl + me;
             const int J = (int)((g - base[x]) / nKq[x]), K = (int)((g - base[x]) % nKq[x]);
-            mt[rnk] = make_int4(J, K, q, 0);
             int m = 0;
             for (int u : dep[t]) {
                 const int pu = local_pos((size_t)u);
                 if (pu < 0 || pu >= rnk) return fail(-1, "tile order not topological");
                 md[(size_t)rnk * ST_MAXDEP + m++] = pu;
             }
+            unsigned dsum = 0;
+            for (int mm = 0; mm < ST_MAXDEP; ++mm) dsum += st_dep_term(mm, md[(size_t)rnk * ST_MAXDEP + mm]);
+            mt[rnk] = make_int4(J, K, q, (int)st_task_check(rnk, J, K, q, W.mgen + 1, dsum));
         }
+        ++W.mgen;
         if (W.cap_mtasks < (size_t)ntasks) {
             (void)hipFree(W.mtasks);
             (void)hipFree(W.mdeps);
@@ -1581,6 +1631,10 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
         }
         W.mkey = key;
     }
+    if (getenv("SDFGEN_DEBUG_VA"))
+        fprintf(stderr, "VA tile multi: mhb [%p, %p) mhc %p mtasks %p mdeps %p mdone %p ctrl %p cell %p\n", (void *)W.mhb,
+                (void *)(W.mhb + W.cap_mhb), (void *)W.mhc, (void *)W.mtasks, (void *)W.mdeps, (void *)W.mdone,
+                (void *)W.ctrl, (void *)cell);
     if (prepare_only) return 0;   // buffers and tables in place (Z-slabs: before anything is enqueued)
     if (++W.mepoch == 0) ++W.mepoch;   // completion flags of this launch (0 = never)
     if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
@@ -1615,6 +1669,7 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     P.deps = W.mdeps;
     P.done = W.mdone;
     P.call_epoch = W.mepoch;
+    P.table_gen = W.mgen;
     P.tm = nsl > 1 ? W.tm : nullptr;
     for (int q = 0; q < ns; ++q) {
         const int sw = s0 + q, *d = dirs[sw % 8];
