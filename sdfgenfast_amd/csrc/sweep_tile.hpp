@@ -1343,6 +1343,8 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     if (++W.epoch == 0) ++W.epoch;   // 0 = never published
     if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     StParams P;
+    memset(&P, 0, sizeof(P));   // every field this launch does not use is null / 0 (P.tm was not: the
+                                // Z-slab launches then added their timers through a stray pointer)
     P.soup = soup;
     P.cell = cell;
     P.hb = W.hb;
@@ -1395,6 +1397,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.hbC = ce - cs;
     P.hc_in = slab.on ? slab.in : nullptr;
     P.hc_out = slab.on ? slab.out : nullptr;
+    P.tm = slab.on ? W.tm : nullptr;
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;

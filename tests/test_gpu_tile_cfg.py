@@ -83,3 +83,13 @@ def test_two_slabs_in_process(cfg, what):
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"), *what],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def test_two_slabs_in_process_per_sweep_launches(cfg):
+    """The Z-slab path with one launch per first-pass sweep (SDFGEN_TILE_MULTI=0: what it falls back
+    to when the overlapped launch's halo buffers do not fit) -- round 4 found these launches adding
+    their phase timers through an uninitialised pointer (an aperture-violation fault)."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="8", SDFGEN_TILE_GRID="96", SDFGEN_TILE_CFG=str(cfg), SDFGEN_TILE_MULTI="0")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"),
+                        "2", "40", "36", "44"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
