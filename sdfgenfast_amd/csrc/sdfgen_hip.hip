@@ -1121,7 +1121,6 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         std::lock_guard<std::mutex> lk(g_prof_mu);
         g_prof = p;
     }
-    if (wf_err & 64) return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep: a task-table row failed its check (table memory corrupted)");
     if (wf_err) {
         st_watchdog_report(ws->wf, "make_level_set3");
         return err.set(SDFGEN_HIP_ERUNTIME, "GPU sweep watchdog fired (lost tile hand-off, code %d)", wf_err);
@@ -1340,9 +1339,6 @@ int slab_alloc(SlabSession *S, Err &err)
     // wrote, mid-kernel.  Whole 2 MiB: a dedicated allocation that IPC maps as is.
     S->cl.init(plane);
     if (int rc = comm_acquire(S->device, S->cl.bytes, &S->comm, err)) return rc;
-    if (getenv("SDFGEN_DEBUG_VA"))
-        fprintf(stderr, "VA slab %d comm [%p, %p) uncached; cell %p\n", S->slab, (void *)S->comm,
-                (void *)(S->comm + S->cl.bytes), (void *)S->cell_mem);
     HIPCHK(hipMemset(S->comm, 0, S->cl.bytes));   // epoch 0 is never published, flags start at 0
     HIPCHK(hipDeviceSynchronize());
     return 0;
@@ -1713,8 +1709,6 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         p.slab_other_tasks = tm[TM_OTHER_TASKS];
         *prof = p;
     }
-    if (wf_err[0] & 64)
-        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: a task-table row failed its check (table memory corrupted)", S->slab);
     if (wf_err[0] & 4)
         return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: upstream slab's plane never arrived (sweep %d)", S->slab,
                        wf_err[1] - 1);

@@ -208,34 +208,9 @@ struct StParams {
     const int *deps;              // [task][ST_MAXDEP]: earlier tasks (previous sweep) to wait for, -1 = none
     unsigned *done;               // [task] = call_epoch once the task's cell stores are visible
     unsigned call_epoch;
-    unsigned table_gen;           // upload count of the tables: part of every row's stamp
     StSweep sw[ST_MAXSW];
     unsigned long long *tm;       // Z-slab phase timers (sweep_sparse.hpp TM_*; null: not recorded)
 };
-
-// Stamp of one row of the multi-sweep task tables (tile_sweep_multi writes it into mtasks[].w):
-// the row's position, its (J, K, slot), a weighted sum of its dependency list and the upload count,
-// so a row left over from an earlier upload does not pass for the current one.
-__host__ __device__ inline unsigned st_task_check(int task, int J, int K, int q, unsigned gen, unsigned dsum)
-{
-    unsigned h = gen * 0x9E3779B1u ^ (unsigned)task * 0x85EBCA77u;
-    h ^= ((unsigned)J << 20) ^ ((unsigned)K << 8) ^ (unsigned)q;
-    h ^= dsum * 0xC2B2AE3Du;
-    h ^= h >> 15;
-    h *= 0x2C1B3C6Du;
-    return h ^ (h >> 13);
-}
-__host__ __device__ inline unsigned st_dep_term(int m, int dep) { return (unsigned)(dep + 1) * (unsigned)(2 * m + 1); }
-
-// Wave-uniform: does this row (tk read by every lane, dep = lane L's dependency) carry its stamp?
-__device__ __forceinline__ bool st_task_row_ok(const StParams &P0, int task, int4 tk, int dep, int L)
-{
-    unsigned d = L < ST_MAXDEP ? st_dep_term(L, dep) : 0u;
-#pragma unroll
-    for (int o = ST_MAXDEP / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
-    d = __shfl(d, 0, 64);
-    return __all((unsigned)tk.w == st_task_check(task, tk.x, tk.y, tk.z, P0.table_gen, d));
-}
 
 __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
 {
@@ -258,21 +233,6 @@ __device__ __forceinline__ void st_fail(const StParams &P, int bit)
     atomicOr(P.err, bit);
     atomicMax(P.err + 1, P.sweep + 1);
     atomicCAS(P.err + 2, 0, (P.sweep + 1) | (bit << 8));   // the first failure: sweep + 1, its bit
-    atomicMax(P.queue, P.ntasks);
-}
-
-// The first failure of a launch also records where a compute wave gave up (ctrl[4..11], read by
-// st_watchdog_report): task, wave, step, own entries ready, prog[w-1], prog[w+1], the lane-min halo
-// readiness of the active lanes and their min a.
-__device__ __forceinline__ void st_fail_at(const StParams &P, int bit, int task, int w, int h, int hx, int pm, int pp,
-                                           int rmin, int amin)
-{
-    atomicOr(P.err, bit);
-    atomicMax(P.err + 1, P.sweep + 1);
-    if (atomicCAS(P.err + 2, 0, (P.sweep + 1) | (bit << 8)) == 0) {
-        const int v[8] = {task, w, h, hx, pm, pp, rmin, amin};
-        for (int q = 0; q < 8; ++q) __hip_atomic_store(P.err + 3 + q, v[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     atomicMax(P.queue, P.ntasks);
 }
 
@@ -356,7 +316,6 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     __shared__ int s_halo_ready[ST_NSTREAM + 1];
     __shared__ int s_abort;
     __shared__ int s_task;
-    __shared__ int4 s_tk;
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -385,28 +344,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         const unsigned long long t_claim = (TRACE && MULTI && P.trace) ? wall_clock64() : 0ull;
         int J, K;
         if (MULTI) {
-            // wave 0 reads the task's row of both tables and checks it against the upload's
-            // stamp (st_task_check); the other waves take (J, K, slot) from LDS.  (Added while
-            // chasing the freed-uncached-memory failure, DESIGN.md §6: the rows were never wrong
-            // there, but a corrupted table would otherwise run wrong tiles silently.)
-            int dep = -1;
-            if (wave == 0) {
-                int4 tk = P0.mtasks[task];
-                dep = L < ST_MAXDEP ? P0.deps[(size_t)task * ST_MAXDEP + L] : -1;
-                if (!st_task_row_ok(P0, task, tk, dep, L)) {
-                    // not the row this launch's upload wrote (the table memory was overwritten or
-                    // read stale): fail loudly rather than run a wrong tile
-                    if (L == 0) {
-                        atomicAdd(P.err + 11, 1);
-                        st_fail(P, 64);
-                    }
-                    tk = make_int4(0, 0, 0, 0);
-                    dep = -1;
-                }
-                if (L == 0) s_tk = tk;
-            }
-            __syncthreads();
-            const int4 tk = s_tk;
+            const int4 tk = P0.mtasks[task];
             J = tk.x;
             K = tk.y;
             const StSweep &sw = P0.sw[tk.z];
@@ -429,6 +367,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             }
             if (wave == 0) {
                 // the previous sweep's tiles under and around this one: their cell stores first
+                const int dep = L < ST_MAXDEP ? P0.deps[(size_t)task * ST_MAXDEP + L] : -1;
                 bool ok = dep < 0;
                 for (unsigned spins = 0;; ++spins) {
                     if (!ok) ok = __hip_atomic_load(P0.done + dep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
@@ -611,16 +550,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     // step is issue-latency bound: -3 % first pass at 256^3)
                     __builtin_amdgcn_s_setprio(0);
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
-                        if (polls > ST_WATCHDOG) {   // this wave gave up (not an abort seen from elsewhere)
-                            const int rmin_ = act ? min(rA, min(rB, rC)) : 0x7fffffff, amin_ = act ? a : 0x7fffffff;
-                            int rm = rmin_, am = amin_;
-#pragma unroll
-                            for (int d_ = 32; d_ >= 1; d_ >>= 1) {
-                                rm = min(rm, __shfl_xor(rm, d_));
-                                am = min(am, __shfl_xor(am, d_));
-                            }
-                            if (L == 0) st_fail_at(P, 2, task, w, h, hx, pm, pp, rm, am);
-                        }
+                        if (polls > ST_WATCHDOG && L == 0) st_fail(P, 2);
                         if (L == 0) lds_st(&s_abort, 1);
                         h = nsteps;
                         break;
@@ -1222,7 +1152,6 @@ struct TileSweepWorkspace {
     double chain_steps = 0.0;   // modelled critical path of that graph, in steps
     int cfg = ST_CFG_LAT;       // the last multi-sweep launch's tile configuration (ST_CFG_*)
     unsigned mepoch = 0;
-    unsigned mgen = 0;     // uploads of the multi-sweep tables (st_task_check)
     int last_ntasks = 0;        // tasks of the last multi-sweep launch (watchdog report) ...
     int last_A = 0, last_B = 0, last_nJ = 0, last_ns = 0, last_nK[ST_MAXSW] = {0}, last_hbC[ST_MAXSW] = {0};
     size_t last_nhb = 0, last_nhc = 0;
@@ -1601,11 +1530,8 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
                 if (pu < 0 || pu >= rnk) return fail(-1, "tile order not topological");
                 md[(size_t)rnk * ST_MAXDEP + m++] = pu;
             }
-            unsigned dsum = 0;
-            for (int mm = 0; mm < ST_MAXDEP; ++mm) dsum += st_dep_term(mm, md[(size_t)rnk * ST_MAXDEP + mm]);
-            mt[rnk] = make_int4(J, K, q, (int)st_task_check(rnk, J, K, q, W.mgen + 1, dsum));
+            mt[rnk] = make_int4(J, K, q, 0);
         }
-        ++W.mgen;
         if (W.cap_mtasks < (size_t)ntasks) {
             (void)hipFree(W.mtasks);
             (void)hipFree(W.mdeps);
@@ -1634,10 +1560,6 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
         }
         W.mkey = key;
     }
-    if (getenv("SDFGEN_DEBUG_VA"))
-        fprintf(stderr, "VA tile multi: mhb [%p, %p) mhc %p mtasks %p mdeps %p mdone %p ctrl %p cell %p\n", (void *)W.mhb,
-                (void *)(W.mhb + W.cap_mhb), (void *)W.mhc, (void *)W.mtasks, (void *)W.mdeps, (void *)W.mdone,
-                (void *)W.ctrl, (void *)cell);
     if (prepare_only) return 0;   // buffers and tables in place (Z-slabs: before anything is enqueued)
     if (++W.mepoch == 0) ++W.mepoch;   // completion flags of this launch (0 = never)
     if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
@@ -1672,7 +1594,6 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     P.deps = W.mdeps;
     P.done = W.mdone;
     P.call_epoch = W.mepoch;
-    P.table_gen = W.mgen;
     P.tm = nsl > 1 ? W.tm : nullptr;
     for (int q = 0; q < ns; ++q) {
         const int sw = s0 + q, *d = dirs[sw % 8];
@@ -1741,10 +1662,6 @@ inline void st_watchdog_report(const TileSweepWorkspace &W, const char *who)
     fprintf(stderr, "%s: tile watchdog: queue %d, error bits %d, max sweep+1 %d, first failure sweep+1 %d bit %d, "
                     "cfg %d, epoch %u, call epoch %u\n", who, ctrl[0], ctrl[1], ctrl[2], ctrl[3] & 0xff, ctrl[3] >> 8, W.cfg,
             W.epoch, W.mepoch);
-    if ((ctrl[3] >> 8) == 2)
-        fprintf(stderr, "  compute wave gave up: task %d wave %d step %d | own ready %d, prog[w-1] %d, prog[w+1] %d, "
-                        "halo ready (lane min) %d, a (lane min) %d\n", ctrl[4], ctrl[5], ctrl[6], ctrl[7], ctrl[8], ctrl[9],
-                ctrl[10], ctrl[11]);
     const int n = W.last_ntasks;
     if (n <= 0 || !W.mdone || !W.mtasks || !W.mdeps) return;
     std::vector<unsigned> done(n);
