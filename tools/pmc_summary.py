@@ -2,7 +2,10 @@
 
 FETCH_SIZE and WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM):
 FETCH_SIZE reports half the bytes of wide coalesced reads -> doubled here; WRITE_SIZE
-is taken as is.  Other access widths are uncalibrated (noted in the output).
+is taken as is.  Round 4 calibrated the widths the tile sweep uses (tools/fetch_calib.hip,
+profiles/r04_fetch_calib.json): FETCH_SIZE counts 64 B per 128-B line for 8- and 16-byte, plain
+and agent-scope loads alike, so the doubling holds for them; WRITE_SIZE counts 32-B granules (an
+8-byte store alone in its line counts 32 B).
 """
 import csv, glob, json, os, sys
 from collections import defaultdict
@@ -50,7 +53,7 @@ for k in sorted(set(fetch) | set(write)):
     kern[k] = {"launches_fetch": len(fetch.get(k, [])), "launches_write": len(write.get(k, [])),
                "fetch_bytes_raw": f, "write_bytes": w, "hbm_bytes_per_launch": int(2 * f + w)}
 res = {"workload": work, "build_id": ids.pop(), "units": "bytes per launch; FETCH_SIZE doubled (gfx950 wide-read correction)",
-       "note": "8-byte and byte-sized accesses are uncalibrated widths; Infinity-Cache hits are counted",
+       "note": "FETCH doubling calibrated for 8- and 16-byte loads (profiles/r04_fetch_calib.json); WRITE_SIZE counts 32-B granules; byte-sized accesses uncalibrated; Infinity-Cache hits are counted",
        "kernels": kern}
 os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
 json.dump(res, open(os.path.join(ROOT, "profiles", "pmc_summary.json"), "w"), indent=1)
