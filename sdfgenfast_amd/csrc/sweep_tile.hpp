@@ -77,6 +77,9 @@ namespace sdfhip {
 #ifndef ST_CSLEEP
 #define ST_CSLEEP 8    // longest back-off of a waiting compute wave
 #endif
+#ifndef ST_QMASK
+#define ST_QMASK 1     // quad tiles: the candidate mask split over the cell's four lanes
+#endif
 #ifndef ST_WPE_DEF
 #define ST_WPE_DEF 3   // waves per SIMD the register budget must allow
 #endif
@@ -597,6 +600,32 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     }
                     // interior cells took part in every earlier sweep (sweep_sparse.hpp: exact skip)
                     const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
+                    if constexpr (Cfg::QUAD && ST_QMASK) {
+                        // The quad splits the test: lane qr decides candidates q = qr and q = qr + 4
+                        // (the 21 pairwise duplicate compares become at most 5 + 8 per lane), and an OR
+                        // over the quad (two DPP moves) gives every lane the cell's mask.  Same rule as
+                        // below, on raw labels (LBL_MASK = none; lbl_of is one-to-one on them).
+                        uint32_t raw[7];
+#pragma unroll
+                        for (int q = 0; q < 7; ++q) raw[q] = (uint32_t)lab[q] & LBL_MASK;
+                        const uint32_t own_raw = own_w & LBL_MASK;
+                        const uint32_t xa = qr == 0 ? raw[0] : qr == 1 ? raw[1] : qr == 2 ? raw[2] : raw[3];
+                        const int la = qr == 0 ? lcq[0] : qr == 1 ? lcq[1] : qr == 2 ? lcq[2] : lcq[3];
+                        const int sa = qr == 0 ? P.seen[0] : qr == 1 ? P.seen[1] : qr == 2 ? P.seen[2] : P.seen[3];
+                        const uint32_t xb = qr == 0 ? raw[4] : qr == 1 ? raw[5] : raw[6];
+                        const int lb = qr == 0 ? lcq[4] : qr == 1 ? lcq[5] : lcq[6];
+                        const int sb = qr == 0 ? P.seen[4] : qr == 1 ? P.seen[5] : P.seen[6];
+                        const bool keep_a = (xa != LBL_MASK) & (xa != own_raw) & !(interior & (la <= sa)) &
+                                            ((qr < 1) | (xa != raw[0])) & ((qr < 2) | (xa != raw[1])) &
+                                            ((qr < 3) | (xa != raw[2]));
+                        const bool keep_b = (qr < 3) & (xb != LBL_MASK) & (xb != own_raw) & !(interior & (lb <= sb)) &
+                                            (xb != raw[0]) & (xb != raw[1]) & (xb != raw[2]) & (xb != raw[3]) &
+                                            ((qr < 1) | (xb != raw[4])) & ((qr < 2) | (xb != raw[5]));
+                        unsigned bits = ((keep_a ? 1u : 0u) << qr) | ((keep_b ? 1u : 0u) << (qr + 4));
+                        bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);   // quad_perm(1,0,3,2)
+                        bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);   // quad_perm(2,3,0,1)
+                        fmask = bits;
+                    } else {
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {   // bitwise, no short-circuit branches
                         bool skip = (lab[q] < 0) | (lab[q] == ct_orig);
@@ -604,6 +633,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         for (int r = 0; r < q; ++r) skip = skip | (lab[r] == lab[q]);
                         skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
                         fmask |= (skip ? 0u : 1u) << q;
+                    }
                     }
                 }
 #ifdef ST_LDS_PROBE   // diagnostics: a dependent chain of N extra LDS reads per compute step
@@ -629,6 +659,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 //      (strict '<', first minimum wins: cpu_lib/makelevelset3.cpp:94-99, 143-149).  A rank
                 //      with no candidate reports NaN, which never passes '<' -- like a skipped check. ----
                     twin_done = true;
+#ifdef ST_STEP_PROF
+                    {
+                        const unsigned long long t_ = clock64();
+                        sp_c[1] += t_ - sp_t;
+                        sp_t = t_;
+                        ++sp_n[!__any(fmask != 0u) ? 0 : (__any(__popc(fmask) > 4u) ? 2 : 1)];
+                    }
+#endif
                     const f3 gx = st_gx(P, a, b, c);
                     const unsigned f1 = fmask & (fmask - 1u), f2 = f1 & (f1 - 1u), f3 = f2 & (f2 - 1u);
                     auto eval_rank = [&](unsigned fr, float &d, int &t, int &e) {
