@@ -77,6 +77,9 @@ namespace sdfhip {
 #ifndef ST_CSLEEP
 #define ST_CSLEEP 8    // longest back-off of a waiting compute wave
 #endif
+#ifndef ST_QMIN
+#define ST_QMIN 1      // quad tiles: a first-minimum reduction over the quad instead of four ordered applies
+#endif
 #ifndef ST_QMASK
 #define ST_QMASK 1     // quad tiles: the candidate mask split over the cell's four lanes
 #endif
@@ -237,6 +240,14 @@ __device__ __forceinline__ void st_fail(const StParams &P, int bit)
     atomicMax(P.err + 1, P.sweep + 1);
     atomicCAS(P.err + 2, 0, (P.sweep + 1) | (bit << 8));   // the first failure: sweep + 1, its bit
     atomicMax(P.queue, P.ntasks);
+}
+
+// v[k] of seven values by a select tree on k's bits (k in 0..6)
+__device__ __forceinline__ int st_sel7(int k, int v0, int v1, int v2, int v3, int v4, int v5, int v6)
+{
+    const bool k0 = k & 1, k1 = k & 2, k2 = k & 4;
+    const int s01 = k0 ? v1 : v0, s23 = k0 ? v3 : v2, s45 = k0 ? v5 : v4;
+    return k2 ? (k1 ? v6 : s45) : (k1 ? s23 : s01);
 }
 
 // low word of a granule published for this sweep (bounded spin; error bit 4 on timeout)
@@ -669,6 +680,60 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #endif
                     const f3 gx = st_gx(P, a, b, c);
                     const unsigned f1 = fmask & (fmask - 1u), f2 = f1 & (f1 - 1u), f3 = f2 & (f2 - 1u);
+#if ST_QMIN
+                    // Each lane evaluates its rank's candidate; a first-minimum reduction over the quad
+                    // (two DPP butterflies) then gives every lane the winner, which is applied once.  Applying
+                    // the ranks one by one with strict '<' (the reference) takes the FIRST candidate whose
+                    // distance is the minimum, if it is below phi: the reduction keeps the earlier rank on
+                    // ties and maps 'no candidate' and NaN distances (which never pass '<') to +inf, which
+                    // never passes '<' either.  The winner's label is read back with its entry at write-back.
+                    const int e0 = ent[0], e1_ = ent[1], e2 = ent[2], e3 = ent[3], e4 = ent[4], e5 = ent[5], e6 = ent[6];
+                    auto eval_rank = [&](unsigned fr, float &key, int &e) {
+                        const bool has = fr != 0u;
+                        const int qa = has ? __builtin_ctz(fr) : 0;
+                        // ent[qa] by a select tree on qa's bits over values, not the array (an indexed
+                        // read of it became a private array promoted to LDS: 9 KB more per tile)
+                        const int e1 = has ? st_sel7(qa, e0, e1_, e2, e3, e4, e5, e6) : e_own;   // no candidate: a valid entry
+                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
+                        const float dd = ptd_wave(gx, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v3),
+                                                  v3.w);
+                        key = (has && dd == dd) ? dd : __builtin_inff();
+                        e = e1;
+                        n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;
+                    };
+                    auto quad_first_min = [&](float &key, int &e) {
+                        // partner lane^1, then lane^2; the lane holding the later rank(s) gives way on ties
+                        float kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false));
+                        int ep = __builtin_amdgcn_mov_dpp(e, 0xB1, 0xf, 0xf, false);
+                        bool take = (qr & 1) ? !(key < kp) : (kp < key);
+                        key = take ? kp : key;
+                        e = take ? ep : e;
+                        kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x4E, 0xf, 0xf, false));
+                        ep = __builtin_amdgcn_mov_dpp(e, 0x4E, 0xf, 0xf, false);
+                        take = (qr & 2) ? !(key < kp) : (kp < key);
+                        key = take ? kp : key;
+                        e = take ? ep : e;
+                    };
+                    if (__any(fmask != 0u)) {
+                        float key;
+                        int e;
+                        eval_rank(qr == 0 ? fmask : (qr == 1 ? f1 : (qr == 2 ? f2 : f3)), key, e);
+                        quad_first_min(key, e);
+                        bool take = key < phi;
+                        phi = take ? key : phi;
+                        win = take ? e : win;
+                        if (__any(__popc(fmask) > 4u)) {   // ranks 4 .. 6 (at most 7 candidates)
+                            const unsigned f4 = f3 & (f3 - 1u), f5 = f4 & (f4 - 1u), f6 = f5 & (f5 - 1u);
+                            eval_rank(qr == 0 ? f4 : (qr == 1 ? f5 : (qr == 2 ? f6 : 0u)), key, e);
+                            quad_first_min(key, e);
+                            take = key < phi;
+                            phi = take ? key : phi;
+                            win = take ? e : win;
+                        }
+                    }
+#else
+                    const f3 gx = st_gx(P, a, b, c);
+                    const unsigned f1 = fmask & (fmask - 1u), f2 = f1 & (f1 - 1u), f3 = f2 & (f2 - 1u);
                     auto eval_rank = [&](unsigned fr, float &d, int &t, int &e) {
                         const bool has = fr != 0u;
                         const int qa = has ? __builtin_ctz(fr) : 0;
@@ -714,6 +779,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         }
                     }
 #undef ST_QB
+#endif
                 } else if constexpr (TWIN) {
                 // ---- candidates in pairs: the cell lane takes the lowest remaining one, its twin
                 //      the next; one ptd per lane per pass, applied in the reference check order
@@ -859,8 +925,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     const float4 w0 = s_ent[__umul24(src, 3)];
                     const float4 w1 = s_ent[__umul24(src, 3) + 1], w2 = s_ent[__umul24(src, 3) + 2];
                     const int slot = ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id;
-                    // a winner always carries a new label (the own label is never a candidate)
-                    const uint32_t w_new = win >= 0 ? lo_word(ct, P.sweep + 1) : own_w;
+                    // a winner always carries a new label (the own label is never a candidate); quad
+                    // tiles (ST_QMIN) take it from the winner's entry, the word its candidate test read
+                    const uint32_t w_new = win < 0 ? own_w
+                                           : (Cfg::QUAD && ST_QMIN) ? lo_word((int)(__float_as_uint(w0.w) & LBL_MASK), P.sweep + 1)
+                                                                    : lo_word(ct, P.sweep + 1);
                     s_ent[__umul24(slot, 3)] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
                     s_ent[__umul24(slot, 3) + 1] = w1;
                     s_ent[__umul24(slot, 3) + 2] = w2;
