@@ -1087,6 +1087,9 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         fprintf(stderr, "step profile: eval cycles per step of the twin path %.0f (%.0f steps), of the compaction path %.0f "
                         "(%.0f steps)\n", wf_stats[12] / std::max(1.0, (double)wf_stats[9]), (double)wf_stats[9],
                 wf_stats[13] / std::max(1.0, (double)wf_stats[10]), (double)wf_stats[10]);
+        fprintf(stderr, "step profile: failed polls %.0f per wave-step: own data not landed %.3f, wave w-1 behind %.3f, "
+                        "wave w+1 ring space %.3f, halo %.3f (a poll can fail on several)\n", wf_stats[1] / steps,
+                wf_stats[3] / steps, wf_stats[14] / steps, (wf_stats[15] & 0xffffffffull) / steps, (wf_stats[15] >> 32) / steps);
     }
 #endif
     p.sweep_evals = wf_stats[0];

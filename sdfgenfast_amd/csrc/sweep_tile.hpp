@@ -520,7 +520,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             unsigned polls = 0;
             unsigned long long t_wait = 0, w_own = 0, w_halo = 0, t_comp = 0, c_comp = 0;   // trace-only
 #ifdef ST_STEP_PROF   // diagnostics: where a compute step's cycles go (host prints the sums)
-            unsigned long long sp_c[4] = {0, 0, 0, 0}, sp_n[4] = {0, 0, 0, 0}, sp_t = 0, sp_ev[2] = {0, 0};
+            unsigned long long sp_c[4] = {0, 0, 0, 0}, sp_n[4] = {0, 0, 0, 0}, sp_t = 0, sp_ev[2] = {0, 0}, sp_pw[3] = {0, 0, 0};
 #endif
             for (int h = 0; h < nsteps; ++h) {
 #ifdef ST_STEP_PROF
@@ -560,6 +560,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     }
                     ++n_cpoll;
                     if (!__all(own_ok)) ++n_cpoll_own;
+#ifdef ST_STEP_PROF
+                    if (!__all((w == 0) | (pm >= h))) ++sp_pw[0];                 // waits on wave w-1
+                    if (!__all((w == ST_NCW - 1) | (pp >= h - P.lead))) ++sp_pw[1];   // ... on wave w+1's ring space
+                    if (!__all(!act | (min(rA, min(rB, rC)) > a))) ++sp_pw[2];     // ... on halo entries
+#endif
                     // a waiting wave yields its SIMD's issue slots to the working waves there (the
                     // step is issue-latency bound: -3 % first pass at 256^3)
                     __builtin_amdgcn_s_setprio(0);
@@ -732,8 +737,6 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         }
                     }
 #else
-                    const f3 gx = st_gx(P, a, b, c);
-                    const unsigned f1 = fmask & (fmask - 1u), f2 = f1 & (f1 - 1u), f3 = f2 & (f2 - 1u);
                     auto eval_rank = [&](unsigned fr, float &d, int &t, int &e) {
                         const bool has = fr != 0u;
                         const int qa = has ? __builtin_ctz(fr) : 0;
@@ -964,6 +967,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 for (int i_ = 0; i_ < 4; ++i_) atomicAdd(P.stats + 8 + i_, sp_n[i_]);
                 atomicAdd(P.stats + 12, sp_ev[0]);
                 atomicAdd(P.stats + 13, sp_ev[1]);
+                atomicAdd(P.stats + 14, sp_pw[0]);
+                atomicAdd(P.stats + 15, sp_pw[1] | (sp_pw[2] << 32));
             }
 #endif
             if (TRACE && P.trace && w == 0 && L == 0) {
