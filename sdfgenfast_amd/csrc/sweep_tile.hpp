@@ -242,6 +242,13 @@ __device__ __forceinline__ void st_fail(const StParams &P, int bit)
     atomicMax(P.queue, P.ntasks);
 }
 
+// v[k] of four values by a select tree on k's bits (k in 0..3)
+__device__ __forceinline__ int st_sel4(int k, int v0, int v1, int v2, int v3)
+{
+    const bool k0 = k & 1, k1 = k & 2;
+    return k1 ? (k0 ? v3 : v2) : (k0 ? v1 : v0);
+}
+
 // v[k] of seven values by a select tree on k's bits (k in 0..6)
 __device__ __forceinline__ int st_sel7(int k, int v0, int v1, int v2, int v3, int v4, int v5, int v6)
 {
@@ -625,12 +632,13 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #pragma unroll
                         for (int q = 0; q < 7; ++q) raw[q] = (uint32_t)lab[q] & LBL_MASK;
                         const uint32_t own_raw = own_w & LBL_MASK;
-                        const uint32_t xa = qr == 0 ? raw[0] : qr == 1 ? raw[1] : qr == 2 ? raw[2] : raw[3];
-                        const int la = qr == 0 ? lcq[0] : qr == 1 ? lcq[1] : qr == 2 ? lcq[2] : lcq[3];
-                        const int sa = qr == 0 ? P.seen[0] : qr == 1 ? P.seen[1] : qr == 2 ? P.seen[2] : P.seen[3];
-                        const uint32_t xb = qr == 0 ? raw[4] : qr == 1 ? raw[5] : raw[6];
-                        const int lb = qr == 0 ? lcq[4] : qr == 1 ? lcq[5] : lcq[6];
-                        const int sb = qr == 0 ? P.seen[4] : qr == 1 ? P.seen[5] : P.seen[6];
+                        // (select trees on qr's bits: nested '?:' on qr compiled to exec-mask branches)
+                        const uint32_t xa = (uint32_t)st_sel4(qr, (int)raw[0], (int)raw[1], (int)raw[2], (int)raw[3]);
+                        const int la = st_sel4(qr, lcq[0], lcq[1], lcq[2], lcq[3]);
+                        const int sa = st_sel4(qr, P.seen[0], P.seen[1], P.seen[2], P.seen[3]);
+                        const uint32_t xb = (uint32_t)st_sel4(qr, (int)raw[4], (int)raw[5], (int)raw[6], (int)raw[6]);
+                        const int lb = st_sel4(qr, lcq[4], lcq[5], lcq[6], lcq[6]);
+                        const int sb = st_sel4(qr, P.seen[4], P.seen[5], P.seen[6], P.seen[6]);
                         const bool keep_a = (xa != LBL_MASK) & (xa != own_raw) & !(interior & (la <= sa)) &
                                             ((qr < 1) | (xa != raw[0])) & ((qr < 2) | (xa != raw[1])) &
                                             ((qr < 3) | (xa != raw[2]));
@@ -704,32 +712,34 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                                                   v3.w);
                         key = (has && dd == dd) ? dd : __builtin_inff();
                         e = e1;
-                        n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;
+                        if (P.stats) n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;   // (counted runs only)
                     };
+                    const bool q_odd = qr & 1, q_hi = qr & 2;
                     auto quad_first_min = [&](float &key, int &e) {
                         // partner lane^1, then lane^2; the lane holding the later rank(s) gives way on ties
                         float kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false));
                         int ep = __builtin_amdgcn_mov_dpp(e, 0xB1, 0xf, 0xf, false);
-                        bool take = (qr & 1) ? !(key < kp) : (kp < key);
+                        // (keys are never NaN: kp <= key is !(key < kp))
+                        bool take = (kp < key) | (q_odd & (kp == key));
                         key = take ? kp : key;
                         e = take ? ep : e;
                         kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x4E, 0xf, 0xf, false));
                         ep = __builtin_amdgcn_mov_dpp(e, 0x4E, 0xf, 0xf, false);
-                        take = (qr & 2) ? !(key < kp) : (kp < key);
+                        take = (kp < key) | (q_hi & (kp == key));
                         key = take ? kp : key;
                         e = take ? ep : e;
                     };
                     if (__any(fmask != 0u)) {
                         float key;
                         int e;
-                        eval_rank(qr == 0 ? fmask : (qr == 1 ? f1 : (qr == 2 ? f2 : f3)), key, e);
+                        eval_rank((unsigned)st_sel4(qr, (int)fmask, (int)f1, (int)f2, (int)f3), key, e);
                         quad_first_min(key, e);
                         bool take = key < phi;
                         phi = take ? key : phi;
                         win = take ? e : win;
                         if (__any(__popc(fmask) > 4u)) {   // ranks 4 .. 6 (at most 7 candidates)
                             const unsigned f4 = f3 & (f3 - 1u), f5 = f4 & (f4 - 1u), f6 = f5 & (f5 - 1u);
-                            eval_rank(qr == 0 ? f4 : (qr == 1 ? f5 : (qr == 2 ? f6 : 0u)), key, e);
+                            eval_rank((unsigned)st_sel4(qr, (int)f4, (int)f5, (int)f6, 0), key, e);
                             quad_first_min(key, e);
                             take = key < phi;
                             phi = take ? key : phi;
