@@ -841,15 +841,24 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             const int i = (int)((unsigned)e % (unsigned)P.ni);
             const unsigned r0 = (unsigned)e / (unsigned)P.ni;
             const int j = (int)(r0 % (unsigned)P.nj), k = (int)(r0 / (unsigned)P.nj);
+            // The upwind words, the cell's current value and its pre-sweep copy are issued together:
+            // ONE round trip (the cell's current value used to be waited for first, then its copy with
+            // the neighbours: two).  Reading sv before knowing the cell moved is safe: whoever changed
+            // the cell stored sv, then X, then fenced before retiring the request we observed.
+            uint32_t w[7];
+            sp_nb_words<true, SLAB>(P, P.X, i, j, k, e, w);
             const unsigned long long cur = sp_ld64(P.X + SDF_CHK(25, e, P.c_lo, P.c_lo + P.n));
+            const unsigned long long pre = P.sv ? sp_ld64(P.sv + e) : P.S[e];
             // f's own input is the cell's pre-sweep value: in place, a cell stamped with this sweep
             // has changed already and keeps it in sv
             const bool moved = P.sv && lc_of((uint32_t)cur) == P.sweep + 1;
 #ifdef SP_NOEVAL_RECHECK   // diagnostics: the work list's own cost (no evaluation, no relabel)
             const unsigned long long y = cur;
+            (void)w;
+            (void)pre;
 #else
-            const unsigned long long own = !P.sv ? P.S[e] : moved ? sp_ld64(P.sv + e) : cur;
-            const unsigned long long y = sp_eval<true, SLAB>(P, P.X, i, j, k, e, own);
+            const unsigned long long own = !P.sv ? pre : moved ? pre : cur;
+            const unsigned long long y = sp_eval_w<true>(P, i, j, k, own, w);
 #endif
             ++runs;
             const bool relabel = y != cur && lbl_of((uint32_t)y) != lbl_of((uint32_t)cur);

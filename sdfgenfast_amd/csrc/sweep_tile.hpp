@@ -243,18 +243,22 @@ __device__ __forceinline__ void st_fail(const StParams &P, int bit)
 }
 
 // v[k] of four values by a select tree on k's bits (k in 0..3)
+// (__builtin_unpredictable: without it the last level became an exec-mask branch)
 __device__ __forceinline__ int st_sel4(int k, int v0, int v1, int v2, int v3)
 {
     const bool k0 = k & 1, k1 = k & 2;
-    return k1 ? (k0 ? v3 : v2) : (k0 ? v1 : v0);
+    const int lo = __builtin_unpredictable(k0) ? v1 : v0, hi = __builtin_unpredictable(k0) ? v3 : v2;
+    return __builtin_unpredictable(k1) ? hi : lo;
 }
 
 // v[k] of seven values by a select tree on k's bits (k in 0..6)
 __device__ __forceinline__ int st_sel7(int k, int v0, int v1, int v2, int v3, int v4, int v5, int v6)
 {
     const bool k0 = k & 1, k1 = k & 2, k2 = k & 4;
-    const int s01 = k0 ? v1 : v0, s23 = k0 ? v3 : v2, s45 = k0 ? v5 : v4;
-    return k2 ? (k1 ? v6 : s45) : (k1 ? s23 : s01);
+    const int s01 = __builtin_unpredictable(k0) ? v1 : v0, s23 = __builtin_unpredictable(k0) ? v3 : v2,
+              s45 = __builtin_unpredictable(k0) ? v5 : v4;
+    const int s03 = __builtin_unpredictable(k1) ? s23 : s01, s47 = __builtin_unpredictable(k1) ? v6 : s45;
+    return __builtin_unpredictable(k2) ? s47 : s03;
 }
 
 // low word of a granule published for this sweep (bounded spin; error bit 4 on timeout)
@@ -598,7 +602,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 polls = 0;
                 // ---- candidates: the 7 upwind labels minus exact duplicates ----
                 float phi = 0.f;
-                int ct = -1, ct_orig = -1, win = -1;
+                int ct = -1, win = -1;
                 uint32_t own_w = 0xffffffffu;
                 int lab[7], ent[7];
                 unsigned fmask = 0;
@@ -608,7 +612,6 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     own_w = __float_as_uint(o0.w);
                     ct = lbl_of(own_w);
                     phi = o1.w;
-                    ct_orig = ct;
                     int lcq[7];
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
@@ -618,7 +621,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         else
                             ent[q] = nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]);
                         const uint32_t wq = __float_as_uint(s_ent[__umul24(ent[q], 3)].w);   // (full-rate 24-bit multiply)
-                        lab[q] = lbl_of(wq);
+                        lab[q] = (int)(wq & LBL_MASK);   // raw (LBL_MASK = none): a candidate is never 'none'
                         lcq[q] = lc_of(wq);
                     }
                     // interior cells took part in every earlier sweep (sweep_sparse.hpp: exact skip)
@@ -630,7 +633,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         // below, on raw labels (LBL_MASK = none; lbl_of is one-to-one on them).
                         uint32_t raw[7];
 #pragma unroll
-                        for (int q = 0; q < 7; ++q) raw[q] = (uint32_t)lab[q] & LBL_MASK;
+                        for (int q = 0; q < 7; ++q) raw[q] = (uint32_t)lab[q];
                         const uint32_t own_raw = own_w & LBL_MASK;
                         // (select trees on qr's bits: nested '?:' on qr compiled to exec-mask branches)
                         const uint32_t xa = (uint32_t)st_sel4(qr, (int)raw[0], (int)raw[1], (int)raw[2], (int)raw[3]);
@@ -652,7 +655,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     } else {
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {   // bitwise, no short-circuit branches
-                        bool skip = (lab[q] < 0) | (lab[q] == ct_orig);
+                        bool skip = (lab[q] == (int)LBL_MASK) | (lab[q] == (int)(own_w & LBL_MASK));   // none, or the own label
 #pragma unroll
                         for (int r = 0; r < q; ++r) skip = skip | (lab[r] == lab[q]);
                         skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
@@ -857,24 +860,22 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 }
 #endif
                 if (single) {
-                    if (fmask) {
-                        int e1 = ent[0], t1 = lab[0];
-#pragma unroll
-                        for (int q = 1; q < 7; ++q)
-                            if (fmask == (1u << q)) {   // static indices: no register-array indexing
-                                e1 = ent[q];
-                                t1 = lab[q];
-                            }
+                    if (__any(fmask != 0u)) {
+                        // the one candidate's entry and label by select trees (an if per slot compiled
+                        // to exec-mask branches); lanes without one evaluate their own entry, unused
+                        const bool has = fmask != 0u;
+                        const int qa = __builtin_ctz(fmask | 0x80u);
+                        const int e1 = has ? st_sel7(qa, ent[0], ent[1], ent[2], ent[3], ent[4], ent[5], ent[6]) : e_own;
+                        const int t1 = st_sel7(qa, lab[0], lab[1], lab[2], lab[3], lab[4], lab[5], lab[6]);
                         const float4 v3 = s_ent[__umul24(e1, 3) + 2];
                         const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]),
                                                st_xyz(v3), v3.w);
-                        if (d < phi) {
-                            phi = d;
-                            ct = t1;
-                            win = e1;
-                        }
+                        const bool take = has & (d < phi);
+                        phi = take ? d : phi;
+                        ct = take ? t1 : ct;
+                        win = take ? e1 : win;
                     }
-                    n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(fmask != 0)) : 0ull;
+                    if (P.stats) n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(fmask != 0)) : 0ull;
                 } else {
                 // ---- compact (cell, candidate) pairs across the wave ----
                 int total = 0;

@@ -169,3 +169,13 @@ def test_gpu_coarse_workloads_match_reference_digest(name):
     assert int(np.count_nonzero(flat < 0)) == rec["inside_lt0"]
     p = _lib.last_profile()
     assert p["band_evals"] > 0
+
+
+def test_gpu_first_call_after_slab_sessions_fresh_process():
+    """Round 4's freed-uncached-memory failure: stage-1 calls, in-process two-slab calls, then the
+    first one-GPU call, in a fresh process (tests/slab_then_one_gpu_check.py)."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_then_one_gpu_check.py")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
