@@ -141,13 +141,15 @@ using StCfgThr = StCfg<1, 4, false, ST_THR_WPE>;
 using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, true>;
 
 enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2 };
-// The configuration of a launch with `tiles` tasks per sweep: the throughput one once a sweep offers
-// more tiles than the chip holds at once (768: 3 per CU), the quad-lane one below (round 4, first
-// pass: 128^3 (256 tiles) 4.78 ms quad vs 5.52 twin lanes; 256^3 (1,024) 12.23-12.30 quad vs
-// 13.73-13.89 twin; 320^3 (1,600) 19.12-19.17 quad vs 18.39-18.45 throughput; 384^3 (2,304) 29.1-29.3
-// vs 23.6-23.9; 512^3 (4,096) 61.1 vs 40.6).  SDFGEN_TILE_CFG=0/1/2 forces one (tests, A/B; 0 = the
-// twin-lane tiles of round 3).
-constexpr long long ST_QUAD_MAX_TILES = 1200;
+// The configuration of a launch with `tiles` tasks per sweep: the quad-lane one while the step
+// latency is what counts, the throughput one once a sweep offers far more tiles than the chip holds
+// at once (768: 3 per CU).  Round 4, first pass, before the quad step's instruction-count work:
+// 128^3 (256 tiles) 4.78 ms quad vs 5.52 twin lanes; 256^3 (1,024) 12.23-12.30 quad vs 13.73-13.89
+// twin; 320^3 (1,600) 19.12-19.17 quad vs 18.39-18.45 throughput; 384^3 (2,304) 29.1-29.3 vs
+// 23.6-23.9; 512^3 (4,096) 61.1 vs 40.6.  After it (select trees etc.): 320^3 16.24
+// quad vs 17.96 throughput, 384^3 24.6-24.7 vs 23.0 -- the crossover moved to between 1,600 and
+// 2,304 tiles.  SDFGEN_TILE_CFG=0/1/2 forces one (tests, A/B; 0 = the twin-lane tiles of round 3).
+constexpr long long ST_QUAD_MAX_TILES = 2000;
 inline int st_cfg(long long tiles)
 {
     if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(2, atoi(e)));
