@@ -334,7 +334,10 @@ def roofline(r, step_us, workload, whole_grid=True):
                "what": "modelled critical path of the launch (tile steps; tile_sweep_multi's schedule) x the "
                        "per-step time of an isolated tile (1024x9x9 grid): the launch time if only the "
                        "dependency chain bounded it"}
-    return {"bound": "latency" if lat else "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+    # "bound" names the roofline the fraction is priced against (the contract's hbm | mfma); what
+    # actually limits the launch is its dependency chain -- "limiter" and the "latency" object say so
+    return {"bound": "hbm", "limiter": "latency (dependency chain)" if lat else None,
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
             "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
             "traffic_source": traffic_src, "kernel": "k_sweep_tile", "sweeps_per_launch": r["sweeps_per_launch"],
             "launches_per_step": r["launches"], "avg_launch_ms": round(r["launch_ms"], 5),
