@@ -69,9 +69,10 @@ def test_full_size_digest(cfg, name):
 
 
 def test_default_selection_by_grid(monkeypatch):
-    """No override: the quad-lane tiles at 256^3 (latency-bound), the 1-wave tiles at 512^3."""
+    """No override: the quad-lane tiles up to 2,000 tiles per sweep (256^3: 1,024; 320^3: 1,600),
+    the 1-wave tiles above (384^3: 2,304; 512^3: 4,096) -- sweep_tile.hpp ST_QUAD_MAX_TILES."""
     monkeypatch.delenv("SDFGEN_TILE_CFG", raising=False)
-    for name, want in (("c3_sphere1m_256", 2), ("c4_sphere1m_512", 1)):
+    for name, want in (("c3_sphere1m_256", 2), ("sphere1m_320", 2), ("sphere1m_384", 1), ("c4_sphere1m_512", 1)):
         v, t, o, dx, dims = meshgen.workload(name)
         _lib.make_level_set3(v, t, o, dx, *dims, 1)
         assert _lib.last_profile()["tile_cfg"] == want, name
