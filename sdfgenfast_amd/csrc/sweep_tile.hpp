@@ -18,9 +18,10 @@
 //     AND the triangle's vertices) live in an LDS ring, so no global load sits on
 //     the critical path.  The ~2 distinct candidates per cell (7 upwind labels minus
 //     duplicates and the cell's own label -- exact skips, see sweep_cell in
-//     sdfgen_hip.hip) are compacted across the wave (ballot + mbcnt) and evaluated
-//     one or two per lane with the branch-free ptd_nb, then each cell applies them
-//     in the reference's check order (strict '<', first minimum wins).
+//     sdfgen_hip.hip) are evaluated by four lanes per cell in one pass (quad tiles) or
+//     compacted across the wave (ballot + mbcnt) and evaluated one or two per lane
+//     (1-wave tiles), then applied in the reference's check order (strict '<', first
+//     minimum wins).
 //   * helper wave: batched, decoupled prefetch.  It streams each column's old
 //     (phi, label) and the label's vertices into an LDS "own" ring, and fills the
 //     17 halo streams (last row of tile J-1, last column of tile K-1, corner) from
@@ -122,8 +123,8 @@ struct StCfg {
     // lead between them (RR = 4 with 2 waves measured wrong results: no lead left).
     static_assert((RR & (RR - 1)) == 0 && (RR >= 8 || (NCW == 1 && RR == 4)), "ring slots: power of two, >= 8 (4 with one compute wave)");
 };
-// Latency-bound grids (few tiles per sweep for the chip, C3): 2 compute waves of 32 cells with twin
-// lanes -- the shortest step; ~47 KB LDS, 3 tiles per CU.  Throughput-bound grids (C4, C5): ONE
+// Round 3's latency-bound tiles (SDFGEN_TILE_CFG=0 only since round 4): 2 compute waves of 32 cells
+// with twin lanes; ~47 KB LDS, 3 tiles per CU.  Throughput-bound grids (C4, C5): ONE
 // compute wave of 64 cells, no ring lead -- half the instructions per cell; ~35 KB LDS, 4 tiles per
 // CU (first pass 512^3: 50.2 -> 44.5 ms, 1024^3: 342 -> 272 ms; 256^3: 13.75 -> 14.6 ms).
 using StCfgLat = StCfg<ST_NCW_DEF, ST_RR_DEF, (ST_TWIN != 0), ST_WPE_DEF>;
@@ -133,8 +134,8 @@ using StCfgLat = StCfg<ST_NCW_DEF, ST_RR_DEF, (ST_TWIN != 0), ST_WPE_DEF>;
 using StCfgThr = StCfg<1, 4, false, ST_THR_WPE>;
 // Latency-bound grids, quad lanes: 4 compute waves of 16 cells, four lanes per cell -- every step
 // evaluates up to 4 candidates per cell in ONE pass (lane 4x + r takes the cell's r-th candidate in
-// check order) and the cell applies them in order from its quad (DPP broadcasts), so no step pays the
-// wave-wide compaction; ~48 KB LDS, 3 tiles per CU (5 waves each: 128 VGPRs).
+// check order) and a first-minimum reduction over the quad combines them, so no step pays the
+// wave-wide compaction; ~43.5 KB LDS, 3 tiles per CU (5 waves each: 128 VGPRs).
 #ifndef ST_QUAD_WPE
 #define ST_QUAD_WPE 4
 #endif
@@ -683,10 +684,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 bool twin_done = false;   // wave-uniform
                 if constexpr (Cfg::QUAD) {
                 // ---- quad lanes: lane r of the cell's quad evaluates the cell's r-th candidate (and, in a
-                //      second pass only for cells with more than 4, its (r+4)-th); the cell lane takes the
-                //      quad's results by DPP broadcasts and applies them in the reference check order
-                //      (strict '<', first minimum wins: cpu_lib/makelevelset3.cpp:94-99, 143-149).  A rank
-                //      with no candidate reports NaN, which never passes '<' -- like a skipped check. ----
+                //      second pass only for cells with more than 4, its (r+4)-th); the quad's results are
+                //      combined as the reference's check order would (strict '<', first minimum wins:
+                //      cpu_lib/makelevelset3.cpp:94-99, 143-149) -- by a first-minimum reduction over the
+                //      quad (ST_QMIN) or, with ST_QMIN=0, by DPP broadcasts applied in rank order.  A rank
+                //      with no candidate never wins -- like a skipped check. ----
                     twin_done = true;
 #ifdef ST_STEP_PROF
                     {
