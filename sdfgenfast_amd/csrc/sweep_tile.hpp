@@ -231,6 +231,14 @@ __device__ __forceinline__ size_t st_inbox(const StParams &P, int a, int b)
 #ifndef ST_FASTFAIL
 #define ST_FASTFAIL 1
 #endif
+
+// Diagnostic builds for the per-buffer traffic split of DESIGN.md §5 (tools/pmc_split.sh): each
+// takes one buffer's accesses off the fabric; the results are wrong, the launch's flow is not.
+//   1: no cell stores   2: own-label vertex gathers read the tile's dummy triangle
+//   3: halo vertex gathers likewise   4: own-cell reads hit the tile's dummy line (and so do 2)
+#ifndef ST_DIAG_SPLIT
+#define ST_DIAG_SPLIT 0
+#endif
 __device__ __forceinline__ bool st_failed(const StParams &P)
 {
     return ST_FASTFAIL && __hip_atomic_load(P.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -951,7 +959,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     s_ent[__umul24(slot, 3)] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
                     s_ent[__umul24(slot, 3) + 1] = w1;
                     s_ent[__umul24(slot, 3) + 2] = w2;
-                    if (win >= 0)
+                    if (win >= 0 && ST_DIAG_SPLIT != 1)
                         P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
                             ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
                     const unsigned long long gran = st_granule(P.epoch, w_new);
@@ -1102,9 +1110,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
 #define ST_GATHER(g, cg, qg)                                                                          \
-    const size_t so##g = 3 * SDF_CHK(11, (ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
+    const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
     const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
-    const size_t sh##g = 3 * SDF_CHK(12, ((g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
+    const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
     const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
                 ST_GATHER(0, c0, q0)
 #ifdef ST_OWNDEDUP   // experiment: slot 1 repeating slot 0's label reads the shared dummy line instead
@@ -1135,7 +1143,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     {                                                                                                  \
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
-        const size_t ix_ = ok_ ? st_phys(P, a_, b, c) : dummy;                                         \
+        const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
         cn = P.cell[SDF_CHK(6, ix_, P.clo, P.chi)];                                                    \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
