@@ -306,6 +306,13 @@ __device__ __forceinline__ f3 st_gx(const StParams &P, int a, int b, int c)
 __device__ __forceinline__ f3 st_xyz(float4 v) { return mk3(v.x, v.y, v.z); }
 
 __device__ __forceinline__ int lds_ld(const int *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+// part k (0..2) of LDS entry e (48 bytes: 3 float4): e a byte offset (EB, the quad tiles) or an index
+template <bool EB>
+__device__ __forceinline__ float4 &st_e(float4 *s_ent, int e, int k)
+{
+    if constexpr (EB) return *(float4 *)((char *)s_ent + e + 16 * k);
+    else return s_ent[__umul24(e, 3) + k];
+}
 __device__ __forceinline__ void lds_st(int *p, int v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 // all of this wave's LDS writes have executed before anything after this point
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -509,10 +516,15 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             const bool col = cell_lane && colx;
             __builtin_amdgcn_s_setprio(ST_WORK_PRIO);
             // neighbour q's entry at step h: nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]) (ring slots are
-            // ST_NCOL = 64 entries apart, halo slots 1)
+            // ST_NCOL = 64 entries apart, halo slots 1); quad tiles keep it as a byte offset (EB below)
             // QUAD (128 VGPRs): ring and halo slots have the same mask (RR == RH), so the shift rides in
             // the base's high bits and the three arrays are one (14 VGPRs fewer)
             constexpr bool NB_PACK = Cfg::QUAD && ST_RR == ST_RH;
+            // the quad tiles address entries by byte offset (one shift-add per neighbour instead of a
+            // shift-add and a multiply: C3 first pass -1.6 %); the others by index (the byte form
+            // measured +0.9 % on the 1-wave tiles at 512^3)
+            constexpr bool EB = NB_PACK;
+            constexpr int ES = EB ? 48 : 1;   // entry stride in the addressing unit
             int nb_base[7], nb_sh[7], nb_mask[7];
             {
                 static_assert(ST_NCOL == 64, "ring slot stride is a shift by 6");
@@ -536,6 +548,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 else if (bl == 0 && cl == 0) { halo(5, 2 * ST_T); halo(6, 2 * ST_T); }
                 else if (bl == 0) { halo(5, cl - 1); halo(6, cl - 1); }
                 else { halo(5, ST_T + bl - 1); halo(6, ST_T + bl - 1); }
+                static_assert(!EB || ST_ENTS * 48 < 65536, "packed byte offsets need 16 bits");
+                if constexpr (EB) {
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) nb_base[q] = ((nb_base[q] & 0xffff) * 48) | (nb_base[q] & ~0xffff);
+                }
             }
             const int hsA = (bl == 0) ? cl : ST_NSTREAM, hsB = (cl == 0) ? ST_T + bl : ST_NSTREAM,
                       hsC = (bl == 0 && cl == 0) ? 2 * ST_T : ST_NSTREAM;
@@ -617,21 +634,22 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 uint32_t own_w = 0xffffffffu;
                 int lab[7], ent[7];
                 unsigned fmask = 0;
-                const int e_own = ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id;
+                const int e_own = __umul24(ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id, ES);
                 if (actx) {
-                    const float4 o0 = s_ent[__umul24(e_own, 3)], o1 = s_ent[__umul24(e_own, 3) + 1];
+                    const float4 o0 = st_e<EB>(s_ent, e_own, 0), o1 = st_e<EB>(s_ent, e_own, 1);
                     own_w = __float_as_uint(o0.w);
                     ct = lbl_of(own_w);
                     phi = o1.w;
                     int lcq[7];
+                    const int t48a = __umul24(a & (ST_RR - 1), 48), t48m = __umul24((a - 1) & (ST_RR - 1), 48);
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
                         const int aq = (q & 1) == 0 ? a - 1 : a;   // q = 0,2,4,6 read a-1
-                        if constexpr (NB_PACK)
-                            ent[q] = (nb_base[q] & 0xffff) + ((aq & (ST_RR - 1)) << (nb_base[q] >> 16));
+                        if constexpr (EB)
+                            ent[q] = (nb_base[q] & 0xffff) + (((q & 1) == 0 ? t48m : t48a) << (nb_base[q] >> 16));
                         else
                             ent[q] = nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]);
-                        const uint32_t wq = __float_as_uint(s_ent[__umul24(ent[q], 3)].w);   // (full-rate 24-bit multiply)
+                        const uint32_t wq = __float_as_uint(st_e<EB>(s_ent, ent[q], 0).w);
                         lab[q] = (int)(wq & LBL_MASK);   // raw (LBL_MASK = none): a candidate is never 'none'
                         lcq[q] = lc_of(wq);
                     }
@@ -722,8 +740,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         // ent[qa] by a select tree on qa's bits over values, not the array (an indexed
                         // read of it became a private array promoted to LDS: 9 KB more per tile)
                         const int e1 = has ? st_sel7(qa, e0, e1_, e2, e3, e4, e5, e6) : e_own;   // no candidate: a valid entry
-                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
-                        const float dd = ptd_wave(gx, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v3),
+                        const float4 v3 = st_e<EB>(s_ent, e1, 2);
+                        const float dd = ptd_wave(gx, st_xyz(st_e<EB>(s_ent, e1, 0)), st_xyz(st_e<EB>(s_ent, e1, 1)), st_xyz(v3),
                                                   v3.w);
                         key = (has && dd == dd) ? dd : __builtin_inff();
                         e = e1;
@@ -772,8 +790,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                             t1 = (qa == q) ? lab[q] : t1;
                         }
                         e1 = has ? e1 : e_own;   // lanes without a candidate read a valid entry
-                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
-                        const float dd = ptd_wave(gx, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v3),
+                        const float4 v3 = st_e<EB>(s_ent, e1, 2);
+                        const float dd = ptd_wave(gx, st_xyz(st_e<EB>(s_ent, e1, 0)), st_xyz(st_e<EB>(s_ent, e1, 1)), st_xyz(v3),
                                                   v3.w);
                         d = has ? dd : __builtin_nanf("");
                         t = t1;
@@ -835,8 +853,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                             e1 = (qa == q) ? ent[q] : e1;
                             t1 = (qa == q) ? lab[q] : t1;
                         }
-                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
-                        const float d1 = ptd_wave(gx, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v3), v3.w);
+                        const float4 v3 = st_e<EB>(s_ent, e1, 2);
+                        const float d1 = ptd_wave(gx, st_xyz(st_e<EB>(s_ent, e1, 0)), st_xyz(st_e<EB>(s_ent, e1, 1)), st_xyz(v3), v3.w);
                         n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;
 #ifdef ST_STEP_PROF
                         ++sp_n[3];
@@ -879,8 +897,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         const int qa = __builtin_ctz(fmask | 0x80u);
                         const int e1 = has ? st_sel7(qa, ent[0], ent[1], ent[2], ent[3], ent[4], ent[5], ent[6]) : e_own;
                         const int t1 = st_sel7(qa, lab[0], lab[1], lab[2], lab[3], lab[4], lab[5], lab[6]);
-                        const float4 v3 = s_ent[__umul24(e1, 3) + 2];
-                        const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]),
+                        const float4 v3 = st_e<EB>(s_ent, e1, 2);
+                        const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(st_e<EB>(s_ent, e1, 0)), st_xyz(st_e<EB>(s_ent, e1, 1)),
                                                st_xyz(v3), v3.w);
                         const bool take = has & (d < phi);
                         phi = take ? d : phi;
@@ -913,15 +931,15 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         const f3 g2 = st_gx(P, h - (l2 & 7) - (ST_CLW * w + (l2 >> 3)), b0 + (l2 & 7),
                                             c0 + ST_CLW * w + (l2 >> 3));
                         float d1, d2;
-                        const float4 v13 = s_ent[__umul24(e1, 3) + 2], v23 = s_ent[__umul24(e2, 3) + 2];
-                        ptd_wave2(g1, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(v13), v13.w, g2,
-                                  st_xyz(s_ent[__umul24(e2, 3)]), st_xyz(s_ent[__umul24(e2, 3) + 1]), st_xyz(v23), v23.w, d1, d2);
+                        const float4 v13 = st_e<EB>(s_ent, e1, 2), v23 = st_e<EB>(s_ent, e2, 2);
+                        ptd_wave2(g1, st_xyz(st_e<EB>(s_ent, e1, 0)), st_xyz(st_e<EB>(s_ent, e1, 1)), st_xyz(v13), v13.w, g2,
+                                  st_xyz(st_e<EB>(s_ent, e2, 0)), st_xyz(st_e<EB>(s_ent, e2, 1)), st_xyz(v23), v23.w, d1, d2);
                         s_pd[w][7 * ST_CPW + ((p1 >> 6) & 7) * ST_CPW + l1] = __float_as_int(d1);
                         s_pd[w][7 * ST_CPW + (has2 ? ((p2 >> 6) & 7) * ST_CPW + l2 : 7 * ST_CPW + L)] = __float_as_int(d2);
                     } else {
                         s_pd[w][7 * ST_CPW + ((p1 >> 6) & 7) * ST_CPW + l1] = __float_as_int(
-                            ptd_wave(g1, st_xyz(s_ent[__umul24(e1, 3)]), st_xyz(s_ent[__umul24(e1, 3) + 1]), st_xyz(s_ent[__umul24(e1, 3) + 2]),
-                                     s_ent[__umul24(e1, 3) + 2].w));
+                            ptd_wave(g1, st_xyz(st_e<EB>(s_ent, e1, 0)), st_xyz(st_e<EB>(s_ent, e1, 1)), st_xyz(st_e<EB>(s_ent, e1, 2)),
+                                     st_e<EB>(s_ent, e1, 2).w));
                     }
                 }
                 n_evals += (L == 0) ? (unsigned long long)total : 0ull;
@@ -948,17 +966,17 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #endif
                 if (act) {
                     const int src = win < 0 ? e_own : win;
-                    const float4 w0 = s_ent[__umul24(src, 3)];
-                    const float4 w1 = s_ent[__umul24(src, 3) + 1], w2 = s_ent[__umul24(src, 3) + 2];
-                    const int slot = ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id;
+                    const float4 w0 = st_e<EB>(s_ent, src, 0);
+                    const float4 w1 = st_e<EB>(s_ent, src, 1), w2 = st_e<EB>(s_ent, src, 2);
+                    const int slot = __umul24(ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id, ES);
                     // a winner always carries a new label (the own label is never a candidate); quad
                     // tiles (ST_QMIN) take it from the winner's entry, the word its candidate test read
                     const uint32_t w_new = win < 0 ? own_w
                                            : (Cfg::QUAD && ST_QMIN) ? lo_word((int)(__float_as_uint(w0.w) & LBL_MASK), P.sweep + 1)
                                                                     : lo_word(ct, P.sweep + 1);
-                    s_ent[__umul24(slot, 3)] = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
-                    s_ent[__umul24(slot, 3) + 1] = w1;
-                    s_ent[__umul24(slot, 3) + 2] = w2;
+                    st_e<EB>(s_ent, slot, 0) = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
+                    st_e<EB>(s_ent, slot, 1) = w1;
+                    st_e<EB>(s_ent, slot, 2) = w2;
                     if (win >= 0 && ST_DIAG_SPLIT != 1)
                         P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
                             ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
