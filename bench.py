@@ -32,6 +32,7 @@ import argparse
 import hashlib
 import json
 import os
+import socket
 import sys
 import time
 
@@ -421,6 +422,18 @@ def main():
         # (3 tile workgroups per CU), or a waiting slab can hold every CU its upstream slab needs.
         os.environ["SDFGEN_TILE_GRID"] = str(max(32, 3 * 256 // ((world + ndev - 1) // ndev) - 32))
     _hiprt.set_device(dev)
+    topo = None
+    if world > 1:
+        # which GPU each rank drives (device, PCI bus id) and the node's peer-access matrix, so that a
+        # mapping failure or watchdog on a multi-GPU node can be tied to the rank pair (the library's
+        # slab errors name slab, device and PCI id of both sides)
+        t = _lib.topology()
+        me = {"rank": rank, "local_rank": local_rank, "device": dev, "host": socket.gethostname(),
+              "pci_bus_id": t["pci_bus_ids"][dev] if dev < len(t["pci_bus_ids"]) else None}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, me)
+        topo = {"ranks": ranks, "devices": t["devices"], "pci_bus_ids": t["pci_bus_ids"],
+                "peer_access": t["peer_access"]}
     step_us = step_latency(dev) if rank == 0 and not args.no_latency else None
 
     res_side = {}
@@ -503,6 +516,8 @@ def main():
             "parity": r["parity"],
             "build_id": _build_id(),
         }
+        if topo:
+            res["topology"] = topo
         if r.get("slab_phases"):
             res["slab_phases"] = r["slab_phases"]   # per rank: where each slab's time went
         res.update(res_side)

@@ -36,7 +36,7 @@ extern "C" {
 /* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
 #pragma GCC visibility push(default)
 
-#define SDFGEN_HIP_ABI_VERSION 3   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers, tile_cfg */
+#define SDFGEN_HIP_ABI_VERSION 4   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers, tile_cfg; 4: sdfgen_hip_topology */
 
 enum {
     SDFGEN_HIP_OK = 0,
@@ -68,6 +68,15 @@ const char *sdfgen_hip_build_id(void);
 /* Number of visible HIP devices (0 when none; never an error).
  * Replaces sdfgen::is_gpu_available() (common/sdfgen_unified.cpp:19-28). */
 int sdfgen_hip_device_count(void);
+
+/* Node topology for the multi-GPU diagnostics (no reference counterpart: the reference has no
+ * multi-GPU layer, README.md:220).  *ndev = visible devices; for the first min(ndev, max_dev):
+ * pci_bus_ids (may be NULL) gets SDFGEN_HIP_PCI_ID_BYTES bytes per device ("0000:05:00.0", NUL
+ * terminated; empty if unknown), peer (may be NULL) a max_dev x max_dev row-major matrix with
+ * peer[i * max_dev + j] = hipDeviceCanAccessPeer(i, j) (1 on the diagonal, -1 if the query failed).
+ * bench.py --gpus N records it with each rank's device. */
+#define SDFGEN_HIP_PCI_ID_BYTES 32
+int sdfgen_hip_topology(int max_dev, int *ndev, char *pci_bus_ids, int *peer);
 
 /*
  * Host-memory entry point; replaces gpu::make_level_set3 (gpu_lib/makelevelset3_gpu.cu:595-777).

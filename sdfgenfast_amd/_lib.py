@@ -28,6 +28,7 @@ EXPORTED = (
     "sdfgen_hip_abi_version",
     "sdfgen_hip_build_id",
     "sdfgen_hip_device_count",
+    "sdfgen_hip_topology",
     "sdfgen_hip_make_level_set3",
     "sdfgen_hip_make_level_set3_device",
     "sdfgen_hip_last_profile",
@@ -113,6 +114,8 @@ def _load():
     L.sdfgen_hip_abi_version.restype = ctypes.c_int
     L.sdfgen_hip_build_id.restype = ctypes.c_char_p
     L.sdfgen_hip_device_count.restype = ctypes.c_int
+    L.sdfgen_hip_topology.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), _P, _P]
+    L.sdfgen_hip_topology.restype = ctypes.c_int
     L.sdfgen_hip_make_level_set3.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
                                              ctypes.c_char_p, ctypes.c_size_t]
@@ -224,6 +227,24 @@ def build_id() -> str:
 
 def device_count() -> int:
     return int(lib.sdfgen_hip_device_count())
+
+
+PCI_ID_BYTES = 32   # SDFGEN_HIP_PCI_ID_BYTES
+
+
+def topology(max_dev: int = 16) -> dict:
+    """sdfgen_hip_topology: the visible devices' PCI bus ids and the hipDeviceCanAccessPeer matrix
+    (bench.py --gpus N records it, so that a mapping failure on a multi-GPU node names the pair)."""
+    n = ctypes.c_int(0)
+    ids = ctypes.create_string_buffer(PCI_ID_BYTES * max_dev)
+    peer = (ctypes.c_int * (max_dev * max_dev))()
+    rc = lib.sdfgen_hip_topology(max_dev, ctypes.byref(n), ids, peer)
+    if rc:
+        raise RuntimeError(f"sdfgen_hip_topology failed ({rc})")
+    m = min(n.value, max_dev)
+    pci = [ids.raw[PCI_ID_BYTES * i:PCI_ID_BYTES * (i + 1)].split(b"\0", 1)[0].decode() for i in range(m)]
+    return {"devices": n.value, "pci_bus_ids": pci,
+            "peer_access": [[int(peer[i * max_dev + j]) for j in range(m)] for i in range(m)]}
 
 
 def make_level_set3(vertices: np.ndarray, triangles: np.ndarray, origin, dx: float, ni: int, nj: int, nk: int,

@@ -292,9 +292,11 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
                     L = LatBox{0, 0, 0, 0};
                 }
             }
-            s_box[tid] = B;
-            s_lat[tid] = L;
-            if (L.nj) {
+            if (tid < BAND_BT) {   // (lanes >= BAND_BT only exist in builds with smaller batches)
+                s_box[tid] = B;
+                s_lat[tid] = L;
+            }
+            if (tid < BAND_BT && L.nj) {
 #pragma unroll
                 for (int c = 0; c < 9; ++c) s_f[tid][c] = f[c];
             }
@@ -1206,8 +1208,28 @@ struct SlabSession {
     int sparse_sweeps = 0, tile_multi = 0;
     hipEvent_t ev[24] = {};
     int launches = 0;
+    int peer_dev[2] = {-1, -1};           // the neighbours' devices (-1: none, or not known for an IPC mapping)
     std::mutex mu;
 };
+
+// "slab s (device d, PCI p; lower slab s-1 on device dl PCI pl; upper ...)": the rank pair a failed
+// hand-off involves, named in slab_finish's errors so that a watchdog on a multi-GPU node is diagnosable
+void slab_where(const SlabSession *S, char *buf, size_t len)
+{
+    auto pci = [](int dev, char *b, size_t n) {
+        if (dev < 0 || hipDeviceGetPCIBusId(b, (int)n, dev) != hipSuccess) snprintf(b, n, "?");
+    };
+    char own[32], lo[32], up[32];
+    pci(S->device, own, sizeof(own));
+    pci(S->peer_dev[0], lo, sizeof(lo));
+    pci(S->peer_dev[1], up, sizeof(up));
+    int n = snprintf(buf, len, "slab %d of %d (device %d, PCI %s", S->slab, S->nslabs, S->device, own);
+    if (S->slab > 0 && n > 0 && (size_t)n < len)
+        n += snprintf(buf + n, len - n, "; lower slab %d on device %d, PCI %s", S->slab - 1, S->peer_dev[0], lo);
+    if (S->slab < S->nslabs - 1 && n > 0 && (size_t)n < len)
+        n += snprintf(buf + n, len - n, "; upper slab %d on device %d, PCI %s", S->slab + 1, S->peer_dev[1], up);
+    if (n > 0 && (size_t)n < len) snprintf(buf + n, len - n, ")");
+}
 
 // Uncached blocks are never returned to the runtime while the process runs.  After hipFree of
 // an uncached (MTYPE UC) block, a later plain hipMalloc that is handed the same virtual range has
@@ -1712,18 +1734,21 @@ int slab_finish(SlabSession *S, uint64_t nvert, sdfgen_hip_profile *prof, Err &e
         p.slab_other_tasks = tm[TM_OTHER_TASKS];
         *prof = p;
     }
-    if (wf_err[0] & 4)
-        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: upstream slab's plane never arrived (sweep %d)", S->slab,
-                       wf_err[1] - 1);
+    char who[256];
+    slab_where(S, who, sizeof(who));
+    if (wf_err[0] & 4) {
+        // the first-pass inbox is written by the slab upstream in the failed sweep's k direction
+        const int sw = wf_err[1] - 1, up = (sw >= 0 && SWEEP_DIRS[sw % 8][2] < 0) ? S->slab + 1 : S->slab - 1;
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU %s: upstream slab %d's plane never arrived (sweep %d)", who, up, sw);
+    }
     if (wf_err[0])
-        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: sweep watchdog fired (lost tile hand-off, code %d, sweep %d)",
-                       S->slab, wf_err[0], wf_err[1] - 1);
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU %s: sweep watchdog fired (lost tile hand-off, code %d, sweep %d)", who,
+                       wf_err[0], wf_err[1] - 1);
     if (sp_ctl[SP_ERR] & 16ull)
-        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: a neighbour slab's second-pass handshake never came", S->slab);
-    if (sp_ctl[SP_ERR] & 8ull)
-        return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: inbound boundary ring overflow", S->slab);
-    if (sp_ctl[SP_ERR] & 4ull) return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: Jacobi list overflow", S->slab);
-    if (sp_ctl[SP_ERR]) return err.set(SDFGEN_HIP_ERUNTIME, "GPU slab %d: sparse sweep watchdog fired", S->slab);
+        return err.set(SDFGEN_HIP_ERUNTIME, "GPU %s: a neighbour slab's second-pass handshake never came", who);
+    if (sp_ctl[SP_ERR] & 8ull) return err.set(SDFGEN_HIP_ERUNTIME, "GPU %s: inbound boundary ring overflow", who);
+    if (sp_ctl[SP_ERR] & 4ull) return err.set(SDFGEN_HIP_ERUNTIME, "GPU %s: Jacobi list overflow", who);
+    if (sp_ctl[SP_ERR]) return err.set(SDFGEN_HIP_ERUNTIME, "GPU %s: sparse sweep watchdog fired", who);
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
                              (unsigned long long)nvert);
     return 0;
@@ -1818,6 +1843,29 @@ extern "C" {
 int sdfgen_hip_abi_version(void) { return SDFGEN_HIP_ABI_VERSION; }
 
 int sdfgen_hip_device_count(void) { return device_count_impl(); }
+
+int sdfgen_hip_topology(int max_dev, int *ndev, char *pci_bus_ids, int *peer)
+{
+    DeviceGuard dg_;
+    if (!ndev || max_dev < 0) return SDFGEN_HIP_EINVAL;
+    const int n = std::max(device_count_impl(), 0);
+    *ndev = n;
+    const int m = std::min(n, max_dev);
+    for (int i = 0; i < m; ++i) {
+        if (pci_bus_ids) {
+            char *b = pci_bus_ids + (size_t)SDFGEN_HIP_PCI_ID_BYTES * i;
+            if (hipDeviceGetPCIBusId(b, SDFGEN_HIP_PCI_ID_BYTES, i) != hipSuccess) b[0] = 0;
+        }
+        if (peer)
+            for (int j = 0; j < m; ++j) {
+                int ok = i == j;
+                if (i != j && hipDeviceCanAccessPeer(&ok, i, j) != hipSuccess) ok = -1;
+                peer[(size_t)i * max_dev + j] = ok;
+            }
+    }
+    (void)hipGetLastError();
+    return 0;
+}
 
 int sdfgen_hip_make_level_set3(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64_t nvert,
                                const float origin[3], float dx, int ni, int nj, int nk, int exact_band, int ngpu,
@@ -2128,6 +2176,21 @@ int sdfgen_hip_slab_connect_ipc(sdfgen_hip_slab *h, const void *lower, const voi
         void *p = nullptr;
         if (int rc = comm_import(S->device, m, &p, err)) return rc;
         S->peer[side] = (char *)p;
+        // Which GPU holds the neighbour's block: checked explicitly, as connect_local does, so a
+        // node whose GPUs cannot reach each other fails here, naming the pair, instead of in a
+        // watchdog mid-sweep.  (A mapping whose owner this process cannot see stays unchecked.)
+        hipPointerAttribute_t pa;
+        int pd = -1;
+        if (hipPointerGetAttributes(&pa, p) == hipSuccess && pa.device >= 0 && pa.device < device_count_impl()) pd = pa.device;
+        (void)hipGetLastError();
+        S->peer_dev[side] = pd;
+        if (pd >= 0 && pd != S->device) {
+            int ok = 0;
+            HIPCHK(hipDeviceCanAccessPeer(&ok, S->device, pd));
+            if (!ok)
+                return err.set(SDFGEN_HIP_ERUNTIME, "slab %d on GPU %d cannot access GPU %d, which holds %s slab %d's inbox",
+                               S->slab, S->device, pd, side ? "upper" : "lower", side ? S->slab + 1 : S->slab - 1);
+        }
         // the mapping must cover the neighbour's whole block (same grid => same layout)
         void *base = nullptr;
         size_t size = 0;
@@ -2160,6 +2223,8 @@ int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *h, sdfgen_hip_slab *lower, sd
     }
     S->peer[0] = lower ? lower->s.comm : nullptr;
     S->peer[1] = upper ? upper->s.comm : nullptr;
+    S->peer_dev[0] = lower ? lower->s.device : -1;
+    S->peer_dev[1] = upper ? upper->s.device : -1;
     return 0;
 }
 

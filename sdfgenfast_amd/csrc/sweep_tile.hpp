@@ -608,7 +608,17 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     // step is issue-latency bound: -3 % first pass at 256^3)
                     __builtin_amdgcn_s_setprio(0);
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
-                        if (polls > ST_WATCHDOG && L == 0) st_fail(P, 2);
+                        if (polls > ST_WATCHDOG) {
+                            // the stuck task and the lowest a still waiting on halo entries, for
+                            // st_watchdog_report: err[3] = task + 1 (the first failure only), err[10] = a + 1
+                            int am = (act && !(min(rA, min(rB, rC)) > a)) ? a : 0x7fffffff;
+#pragma unroll
+                            for (int d_ = 1; d_ < 64; d_ <<= 1) am = min(am, __shfl_xor(am, d_));
+                            if (L == 0) {
+                                if (atomicCAS(P.err + 3, 0, task + 1) == 0) atomicExch(P.err + 10, am == 0x7fffffff ? 0 : am + 1);
+                                st_fail(P, 2);
+                            }
+                        }
                         if (L == 0) lds_st(&s_abort, 1);
                         h = nsteps;
                         break;
@@ -1844,7 +1854,8 @@ inline void st_watchdog_report(const TileSweepWorkspace &W, const char *who)
         ++shown;
     }
     // the stuck compute wave's halo entries at a = amin: the granules the helper polls
-    const int task = ctrl[4], amin = ctrl[11];
+    // (k_sweep_tile's compute-wave watchdog records them: err[3] = ctrl[4] = task + 1, err[10] = ctrl[11] = a + 1)
+    const int task = ctrl[4] - 1, amin = ctrl[11] - 1;
     if ((ctrl[3] >> 8) == 2 && task >= 0 && task < n && amin >= 0 && amin < W.last_A) {
         const int J = tk[task].x, K = tk[task].y, q = tk[task].z;
         const unsigned eq = W.epoch - (unsigned)(W.last_ns - 1 - q);   // slot q's epoch (one per sweep, in order)

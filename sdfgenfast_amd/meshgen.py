@@ -133,17 +133,32 @@ def tetrahedron():
     return v, t
 
 
-def x3y4z5():
-    """The reference's benchmark mesh tests/resources/test_x3y4z5_bin.stl (36 triangles; stored as data
-    in tests/golden/resources), loaded with the native loader (bit-identical to the reference's
-    meshio::load_stl, tests/test_meshio_ref.py)."""
-    import os
+# The reference's benchmark mesh tests/resources/test_x3y4z5_bin.stl as data: 36 triangles, 108 unshared
+# vertices in file order (the binary STL's vertex coordinates are small integers), so the package needs no
+# test tree (tests/test_api.py checks it against the loader on tests/golden/resources/test_x3y4z5_bin.stl).
+_X3Y4Z5_XYZ = (
+    -1, -1, -1, -1, -1, 1, -1, 1, 1, -1, -1, -1, -1, 1, 1, -1, 1, -1, -1, 1, 1, 1, 1, 1, 1, 3, 1,
+    -1, 1, 1, 1, 3, 1, -1, 3, 1, 1, -1, 1, 1, -1, -1, 2, -1, -1, 1, -1, 1, 2, -1, -1, 2, -1, 1,
+    1, -1, -1, 1, -1, 1, -1, -1, 1, 1, -1, -1, -1, -1, 1, -1, -1, -1, -1, 1, -1, 1, 1, -1, 1, -1, -1,
+    -1, 1, -1, 1, -1, -1, -1, -1, -1, 1, 1, 1, -1, 1, 1, -1, 1, 4, 1, 1, 1, -1, 1, 4, 1, 1, 4,
+    2, 1, -1, 2, 1, 1, 2, -1, 1, 2, 1, -1, 2, -1, 1, 2, -1, -1, 1, -1, -1, 1, 1, -1, 2, 1, -1,
+    1, -1, -1, 2, 1, -1, 2, -1, -1, 1, 1, 1, 1, -1, 1, 2, -1, 1, 1, 1, 1, 2, -1, 1, 2, 1, 1,
+    1, 1, -1, 1, 1, 1, 2, 1, 1, 1, 1, -1, 2, 1, 1, 2, 1, -1, -1, 3, -1, -1, 3, 1, 1, 3, 1,
+    -1, 3, -1, 1, 3, 1, 1, 3, -1, -1, 1, -1, -1, 1, 1, -1, 3, 1, -1, 1, -1, -1, 3, 1, -1, 3, -1,
+    1, 1, 1, 1, 1, -1, 1, 3, -1, 1, 1, 1, 1, 3, -1, 1, 3, 1, 1, 1, -1, -1, 1, -1, -1, 3, -1,
+    1, 1, -1, -1, 3, -1, 1, 3, -1, 1, 1, 4, -1, 1, 4, -1, -1, 4, 1, 1, 4, -1, -1, 4, 1, -1, 4,
+    1, -1, 1, 1, 1, 1, 1, 1, 4, 1, -1, 1, 1, 1, 4, 1, -1, 4, -1, 1, 1, -1, -1, 1, -1, -1, 4,
+    -1, 1, 1, -1, -1, 4, -1, 1, 4, -1, -1, 1, 1, -1, 1, 1, -1, 4, -1, -1, 1, 1, -1, 4, -1, -1, 4,
+)
 
-    from . import meshio
-    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
-                        "resources", "test_x3y4z5_bin.stl")
-    v, t = meshio.load_mesh(path)[:2]
-    return np.ascontiguousarray(v, np.float32), np.ascontiguousarray(t, np.uint32)
+
+def x3y4z5():
+    """The reference's benchmark mesh tests/resources/test_x3y4z5_bin.stl (36 triangles), embedded: the
+    vertices and faces the native loader returns for that file (bit-identical to the reference's
+    meshio::load_stl, tests/test_meshio_ref.py)."""
+    v = np.array(_X3Y4Z5_XYZ, np.float32).reshape(-1, 3)
+    t = np.arange(v.shape[0], dtype=np.uint32).reshape(-1, 3)
+    return v, t
 
 
 # Named workloads: BASELINE.json's configs (SURVEY 8.d table), the reference's own published benchmark

@@ -6,6 +6,9 @@ GPU_MAX_HW_QUEUES raised, so that every slab's stream gets its own hardware queu
 test_gpu_slab.py for why); SDFGEN_LIB_OVERRIDE selects the bounds-checked library.
     python tests/slab_inprocess_check.py NSLABS NI NJ NK
     python tests/slab_inprocess_check.py NSLABS WORKLOAD [REPS]
+    python tests/slab_inprocess_check.py NSLABS WORKLOAD REPS --cabi
+The --cabi form runs the split through sdfgen_hip_make_level_set3(ngpu = NSLABS) -- the C-ABI's own
+multi-device path -- with every slab on device 0 (SDFGEN_DEBUG_SLABS_ONE_DEVICE) and host arrays.
 """
 import hashlib
 import json
@@ -38,6 +41,22 @@ def main():
             rec = json.load(f)[name]
         want = None
     print(f"library {os.path.basename(_lib.LIB_PATH)} build {_lib.build_id()}", flush=True)
+    if "--cabi" in sys.argv:
+        if rec is None:
+            print("ERROR --cabi needs a named workload")
+            return 1
+        os.environ["SDFGEN_DEBUG_SLABS_ONE_DEVICE"] = "1"
+        for rep in range(reps):
+            phi = _lib.make_level_set3(v, t, o, dx, ni, nj, nk, 1, _lib.LAYOUT_ARRAY3, ngpu=nslabs)
+            raw = np.asarray(phi, np.float32).ravel(order="F")   # i-fastest, the Array3f bytes
+            got = hashlib.sha256(raw.astype("<f4", copy=False).tobytes()).hexdigest()
+            inside = int(np.count_nonzero(raw < 0))
+            if got != rec["sha256_phi"] or inside != rec["inside_lt0"]:
+                print(f"MISMATCH {name} (C-ABI ngpu={nslabs}): sha256 {got[:16]} inside {inside} vs reference "
+                      f"{rec['sha256_phi'][:16]} {rec['inside_lt0']}")
+                return 1
+        print(f"OK {nslabs} slabs {name} x{reps} (C-ABI ngpu)")
+        return 0
     slabs = [_lib.Slab(0, nslabs, s, ni, nj, nk) for s in range(nslabs)]
     for s, sl in enumerate(slabs):
         sl.connect_local(slabs[s - 1] if s > 0 else None, slabs[s + 1] if s < nslabs - 1 else None)

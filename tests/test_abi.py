@@ -50,8 +50,15 @@ def test_build_id_matches_sources():
 
 
 def test_abi_version_and_device_count():
-    assert _lib.lib.sdfgen_hip_abi_version() == 3
+    assert _lib.lib.sdfgen_hip_abi_version() == 4
     assert _lib.device_count() >= 0
+
+
+def test_topology_without_gpu_is_empty_not_an_error():
+    t = _lib.topology()
+    assert t["devices"] == _lib.device_count()
+    assert len(t["pci_bus_ids"]) == min(t["devices"], 16) and len(t["peer_access"]) == len(t["pci_bus_ids"])
+    assert all(t["peer_access"][i][i] == 1 for i in range(len(t["peer_access"])))
 
 
 def test_argument_validation_without_gpu():

@@ -294,3 +294,16 @@ def test_reference_stl_and_obj_resources_load():
     z = np.load(os.path.join(os.path.dirname(__file__), "golden", "cases.npz"))
     v = z["x3y4z5_stl_32/vertices"]
     assert v.shape == (108, 3)   # binary STL: no de-duplication (mesh_io_stl.cpp:157-165)
+
+
+def test_embedded_x3y4z5_mesh_matches_the_stl_file():
+    """meshgen.x3y4z5() ships the reference's benchmark mesh as data (no test tree needed at run
+    time); it must be exactly what the native loader reads from the STL file."""
+    import os
+
+    from sdfgenfast_amd import meshgen, meshio
+    path = os.path.join(os.path.dirname(__file__), "golden", "resources", "test_x3y4z5_bin.stl")
+    v, t = meshio.load_mesh(path)[:2]
+    ev, et = meshgen.x3y4z5()
+    assert ev.dtype == np.float32 and et.dtype == np.uint32
+    assert np.array_equal(ev, np.asarray(v, np.float32)) and np.array_equal(et, np.asarray(t, np.uint32))

@@ -131,6 +131,22 @@ def test_two_slabs_full_size_match_reference_digest(name):
     assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
 
 
+@pytest.mark.parametrize("name,mode", [("c2_sphere70k_128", "slabs"), ("c2_sphere70k_128", "cabi"),
+                                       ("c4_sphere1m_512", "slabs")])
+def test_eight_slabs_in_process_match_reference_digest(name, mode):
+    """north_star's 8-way Z split (C4 names 8 GPUs): eight slabs of one grid on this box's one GPU in
+    one process -- every slab with both neighbours but the ends, seven slab boundaries per sweep --
+    against the reference's SHA-256 of phi.  `slabs`: the slab C-ABI driven per slab (8 streams, one
+    hardware queue each); `cabi`: sdfgen_hip_make_level_set3(ngpu=8), the library's own in-process
+    multi-device path, with SDFGEN_DEBUG_SLABS_ONE_DEVICE.  The persistent tile grids are capped
+    (48 workgroups per slab) so that all eight slabs stay co-resident; on 8 GPUs nothing is shared."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", SDFGEN_TILE_GRID="48")
+    args = ["8", name, "2" if name.startswith("c2") else "1"] + (["--cabi"] if mode == "cabi" else [])
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"), *args],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "\nOK " in "\n" + r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
 # One process per slab, inboxes mapped with HIP IPC.  Two processes only: more processes
 # sharing one GPU's hardware queues are not guaranteed to run their kernels concurrently.
 @pytest.mark.parametrize("nslabs,dims", [(2, (40, 36, 44)), (2, (19, 23, 31))])

@@ -13,6 +13,7 @@
 #   prof=WORKLOAD    the same on another workload
 #   pmc              HBM + SQ counter passes on C3 (tools/pmc.sh, tools/pmc_sq.sh)
 #   py=SCRIPT,ARGS   python3 SCRIPT ARGS (a tools/ script)           -> gpurun_out/TAG_py<n>.log
+#   exe=PROG,ARGS    a probe built here (tools/uc_free_probe,3)      -> gpurun_out/TAG_exe<n>.log
 #                    (py=tools/fuzz_parity.py,200,3033  py=tools/c5_time.py  py=tools/wl_check.py,x3y4z5_prop256)
 #   nrank=N          bench.py --gpus N under torch.distributed.run with all N ranks on this box's ONE GPU:
 #                    a rehearsal of the Z-slab path (bit-exact check), not a scaling figure
@@ -71,6 +72,9 @@ for s in "$@"; do
   py=*)
     a=${s#py=}
     run "${TAG}_py$n.log" 900 python3 ${a//,/ } ;;
+  exe=*)
+    a=${s#exe=}
+    run "${TAG}_exe$n.log" 300 ${a//,/ } ;;
   *) echo "unknown step $s"; exit 2 ;;
   esac
 done
