@@ -98,15 +98,17 @@ static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of 
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
 
 // Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, the waves
-// per SIMD the register budget must allow, and quad lanes.
-template <int NCW_, int RR_, bool TWIN_, int WPE_, bool QUAD_ = false>
+// per SIMD the register budget must allow, and lanes per cell (4: quad lanes, 2: duo lanes).
+template <int NCW_, int RR_, bool TWIN_, int WPE_, int LPC_ = 1>
 struct StCfg {
     static constexpr int NCW = NCW_;                    // compute waves per tile
     static constexpr int CLW = ST_T / NCW;              // c-columns per compute wave
     static constexpr int CPW = ST_T * CLW;              // cells per compute wave
     static constexpr int RR = RR_;                      // neighbour ring slots
     static constexpr bool TWIN = TWIN_;                 // lane L + 32 is the twin of cell lane L
-    static constexpr bool QUAD = QUAD_;                 // four lanes per cell: lanes 4x .. 4x + 3 are cell x
+    static constexpr int LPC = LPC_;                    // lanes per cell: lanes LPC x .. LPC x + LPC - 1 are cell x
+    static constexpr bool QUAD = LPC_ > 1;              // the lanes-per-cell step (quad or duo lanes): no compaction
+    static constexpr int LPC_SH = LPC_ == 4 ? 2 : (LPC_ == 2 ? 1 : 0);
     static constexpr int WPE = WPE_;
     static constexpr int LEAD = NCW > 1 ? RR - 4 : 0;   // max lead of wave w over wave w+1 (ring hazard)
     static constexpr int THREADS = 64 * (NCW + 1);      // compute waves + helper wave
@@ -117,7 +119,8 @@ struct StCfg {
     static_assert(NCW >= 1 && NCW <= 4 && ST_T % NCW == 0, "compute waves must split the tile's c-columns");
     static_assert(NCW <= 3 || QUAD, "four compute waves: the quad-lane step only");
     static_assert(!TWIN || CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
-    static_assert(!QUAD || (CPW == 16 && !TWIN), "quad lanes: a compute wave owns 16 cells, 4 lanes each");
+    static_assert(LPC == 1 || LPC == 2 || LPC == 4, "lanes per cell: 1, 2 or 4");
+    static_assert(!QUAD || (CPW * LPC == 64 && !TWIN), "lanes per cell: a compute wave owns 64 / LPC cells");
     // Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
     // neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the
     // lead between them (RR = 4 with 2 waves measured wrong results: no lead left).
@@ -139,9 +142,18 @@ using StCfgThr = StCfg<1, 4, false, ST_THR_WPE>;
 #ifndef ST_QUAD_WPE
 #define ST_QUAD_WPE 4
 #endif
-using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, true>;
+using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, 4>;
+// Duo lanes (round 5): 2 compute waves of 32 cells, two lanes per cell -- lane 2x + r evaluates the
+// cell's candidates of rank r, r + 2, ... in passes of one ptd_wave each (a second pass only when a cell
+// of the wave has more than 2 candidates), a first-minimum reduction over the pair (one DPP move).  Half
+// the compute waves of the quad tiles per step, so two tiles' compute waves share a SIMD's issue slots
+// less; ~43 KB LDS, 3 tiles per CU (3 waves each: 168 VGPRs).
+#ifndef ST_DUO_WPE
+#define ST_DUO_WPE 3
+#endif
+using StCfgDuo = StCfg<2, 8, false, ST_DUO_WPE, 2>;
 
-enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2 };
+enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3 };
 // The configuration of a launch with `tiles` tasks per sweep: the quad-lane one while the step
 // latency is what counts, the throughput one once a sweep offers far more tiles than the chip holds
 // at once (768: 3 per CU).  Round 4, first pass, before the quad step's instruction-count work:
@@ -153,7 +165,7 @@ enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2 };
 constexpr long long ST_QUAD_MAX_TILES = 2000;
 inline int st_cfg(long long tiles)
 {
-    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(2, atoi(e)));
+    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(3, atoi(e)));
     return tiles > ST_QUAD_MAX_TILES ? ST_CFG_THR : ST_CFG_QUAD;
 }
 inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
@@ -344,13 +356,12 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     StParams P = P0;
     constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
-    // per compute wave: (entry << 9 | q << 6 | lane) list, then one trash word per lane (the
-    // target of lanes with nothing to store, so the stores need no divergent branch)
+    // per compute wave (not used by the lanes-per-cell step: one word then):
     // s_pd[w]: [0, 7 CPW) the (entry << 9 | q << 6 | lane) list, [7 CPW, 14 CPW) the distance bits of
     // candidate q for lane (q * CPW + lane), then ONE trash word per lane shared by both (the target of
     // lanes with nothing to store, so the stores need no divergent branch; one trash area instead of
     // two leaves room for a 16-slot halo ring at 3 tiles per CU)
-    __shared__ int s_pd[ST_NCW][14 * ST_CPW + 64];
+    __shared__ int s_pd[ST_NCW][Cfg::QUAD ? 1 : 14 * ST_CPW + 64];
     // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
     // compute wave w.
     __shared__ __attribute__((aligned(16))) int s_hdr[ST_NCW < 4 ? 4 : 8];
@@ -506,8 +517,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             const int w = wave;
             // lane -> cell: cell lanes 0 .. CPW-1 (TWIN: lane L + 32 the twin of L); QUAD: cell x is lanes
             // 4x .. 4x + 3, the lane's rank qr = L & 3, and lane 4x applies and stores
-            const int lcell = Cfg::QUAD ? (L >> 2) : L;
-            const int qr = Cfg::QUAD ? (L & 3) : 0;
+            const int lcell = L >> Cfg::LPC_SH;
+            const int qr = L & (Cfg::LPC - 1);
             const bool cell_lane = Cfg::QUAD ? (qr == 0) : (L < ST_CPW);
             const int bl = lcell & (ST_T - 1), cl = ST_CLW * w + ((lcell >> 3) & (ST_CLW - 1));
             const int col_id = cl * ST_T + bl;
@@ -665,7 +676,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     }
                     // interior cells took part in every earlier sweep (sweep_sparse.hpp: exact skip)
                     const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
-                    if constexpr (Cfg::QUAD && ST_QMASK) {
+                    if constexpr (Cfg::LPC == 4 && ST_QMASK) {
                         // The quad splits the test: lane qr decides candidates q = qr and q = qr + 4
                         // (the 21 pairwise duplicate compares become at most 5 + 8 per lane), and an OR
                         // over the quad (two DPP moves) gives every lane the cell's mask.  Same rule as
@@ -690,6 +701,29 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         unsigned bits = ((keep_a ? 1u : 0u) << qr) | ((keep_b ? 1u : 0u) << (qr + 4));
                         bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);   // quad_perm(1,0,3,2)
                         bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);   // quad_perm(2,3,0,1)
+                        fmask = bits;
+                    } else if constexpr (Cfg::LPC == 2 && ST_QMASK) {
+                        // Duo lanes: lane qr decides candidates q = qr, qr + 2, qr + 4 (and lane 0 also q = 6),
+                        // an OR with the partner lane (one DPP move) gives both the cell's mask.
+                        uint32_t raw[7];
+#pragma unroll
+                        for (int q = 0; q < 7; ++q) raw[q] = (uint32_t)lab[q];
+                        const uint32_t own_raw = own_w & LBL_MASK;
+                        const bool q1 = qr & 1;
+                        const uint32_t xa = q1 ? raw[1] : raw[0], xb = q1 ? raw[3] : raw[2], xc = q1 ? raw[5] : raw[4], xd = raw[6];
+                        const int la = q1 ? lcq[1] : lcq[0], lb = q1 ? lcq[3] : lcq[2], lc = q1 ? lcq[5] : lcq[4];
+                        const int sa = q1 ? P.seen[1] : P.seen[0], sb = q1 ? P.seen[3] : P.seen[2], sc = q1 ? P.seen[5] : P.seen[4];
+                        const bool keep_a = (xa != LBL_MASK) & (xa != own_raw) & !(interior & (la <= sa)) & (!q1 | (xa != raw[0]));
+                        const bool keep_b = (xb != LBL_MASK) & (xb != own_raw) & !(interior & (lb <= sb)) & (xb != raw[0]) &
+                                            (xb != raw[1]) & (!q1 | (xb != raw[2]));
+                        const bool keep_c = (xc != LBL_MASK) & (xc != own_raw) & !(interior & (lc <= sc)) & (xc != raw[0]) &
+                                            (xc != raw[1]) & (xc != raw[2]) & (xc != raw[3]) & (!q1 | (xc != raw[4]));
+                        const bool keep_d = !q1 & (xd != LBL_MASK) & (xd != own_raw) & !(interior & (lcq[6] <= P.seen[6])) &
+                                            (xd != raw[0]) & (xd != raw[1]) & (xd != raw[2]) & (xd != raw[3]) & (xd != raw[4]) &
+                                            (xd != raw[5]);
+                        unsigned bits = ((keep_a ? 1u : 0u) << qr) | ((keep_b ? 1u : 0u) << (qr + 2)) |
+                                        ((keep_c ? 1u : 0u) << (qr + 4)) | ((keep_d ? 1u : 0u) << 6);
+                        bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);   // quad_perm(1,0,3,2)
                         fmask = bits;
                     } else {
 #pragma unroll
@@ -758,6 +792,29 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         if (P.stats) n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(has)) : 0ull;   // (counted runs only)
                     };
                     const bool q_odd = qr & 1, q_hi = qr & 2;
+                    if constexpr (Cfg::LPC == 2) {
+                        // duo lanes: pass p evaluates ranks 2p (lane 0) and 2p + 1 (lane 1); the pair's first
+                        // minimum (lane 1 gives way on ties) is applied after each pass with strict '<', so an
+                        // earlier pass keeps ties -- the reference's check order, pass after pass
+                        if (__any(fmask != 0u)) {
+                            unsigned fr = fmask;   // the candidates not yet evaluated
+                            do {
+                                const unsigned fq = fr & (fr - 1u);
+                                float key;
+                                int e;
+                                eval_rank(q_odd ? fq : fr, key, e);
+                                const float kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false));
+                                const int ep = __builtin_amdgcn_mov_dpp(e, 0xB1, 0xf, 0xf, false);
+                                const bool tp = (kp < key) | (q_odd & (kp == key));
+                                key = tp ? kp : key;
+                                e = tp ? ep : e;
+                                const bool take = key < phi;
+                                phi = take ? key : phi;
+                                win = take ? e : win;
+                                fr = fq & (fq - 1u);
+                            } while (__any(fr != 0u));
+                        }
+                    } else {
                     auto quad_first_min = [&](float &key, int &e) {
                         // partner lane^1, then lane^2; the lane holding the later rank(s) gives way on ties
                         float kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false));
@@ -789,7 +846,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                             win = take ? e : win;
                         }
                     }
+                    }   // LPC == 4
 #else
+                    static_assert(Cfg::LPC == 4, "duo lanes: the first-minimum reduction only (ST_QMIN)");
                     auto eval_rank = [&](unsigned fr, float &d, int &t, int &e) {
                         const bool has = fr != 0u;
                         const int qa = has ? __builtin_ctz(fr) : 0;
@@ -888,7 +947,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     fmask = cell_lane ? fmask : 0u;   // the compaction below lists each cell's pairs once
                 }
                 }
-                if (!twin_done) {
+                if (!Cfg::QUAD && !twin_done) {
                 // ---- at most one candidate per cell (the common case away from the surface):
                 //      each cell lane evaluates its own, no compaction and no LDS exchange ----
                 const bool single = __all(__popc(fmask) <= 1);
@@ -1414,6 +1473,7 @@ inline void st_launch(int cfg, int grid, hipStream_t st, StParams &P, int lead_o
 {
     if (cfg == ST_CFG_THR) st_launch_cfg<StCfgThr, SLAB, TRACE, MULTI>("thr", grid, st, P, lead_override);
     else if (cfg == ST_CFG_QUAD) st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
+    else if (cfg == ST_CFG_DUO) st_launch_cfg<StCfgDuo, SLAB, TRACE, MULTI>("duo", grid, st, P, lead_override);
     else st_launch_cfg<StCfgLat, SLAB, TRACE, MULTI>("lat", grid, st, P, lead_override);
 }
 

@@ -1,4 +1,4 @@
-"""The first-pass tile kernel configurations (sweep_tile.hpp StCfgLat / StCfgThr / StCfgQuad) against
+"""The first-pass tile kernel configurations (sweep_tile.hpp StCfgLat / StCfgThr / StCfgQuad / StCfgDuo) against
 the oracle and the reference digests.  The library picks one by the tiles a sweep offers (st_use_thr:
 256^3 runs the 2-wave tiles, 512^3 and 1024^3 the 1-wave tiles); SDFGEN_TILE_CFG forces either, so
 each is pinned on every grid shape here -- ragged, tiny, shifted, full size and Z-slabs."""
@@ -16,10 +16,10 @@ from oracle import oracle as O
 from sdfgenfast_amd import _lib, meshgen
 
 pytestmark = pytest.mark.gpu
-CFGS = [0, 1, 2]
+CFGS = [0, 1, 2, 3]
 
 
-@pytest.fixture(params=CFGS, ids=["lat", "thr", "quad"])
+@pytest.fixture(params=CFGS, ids=["lat", "thr", "quad", "duo"])
 def cfg(request, monkeypatch):
     monkeypatch.setenv("SDFGEN_TILE_CFG", str(request.param))
     return request.param
