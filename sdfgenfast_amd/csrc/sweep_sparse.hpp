@@ -103,6 +103,10 @@ constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup
 #define SP_LOCAL_LANES 32   // k_sp_recheck: lanes per wave that take no ring tickets (sp_hand_local)
 #endif
 static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least one ring lane");
+#ifndef SP_DIRECT_POLL
+#define SP_DIRECT_POLL 1   // k_sp_recheck: a waiting ring lane polls its slot in the same round trip as the
+                           // wave's tail read (the tail only decides the shard's drain), not after it
+#endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
@@ -770,6 +774,11 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             }
         }
         SP_IP(0);
+        // SP_DIRECT_POLL: a waiting ring lane's slot poll is issued first, so that it and the tail read
+        // below share one round trip (the tail then only decides the shard's drain)
+        unsigned vpoll = 0u;
+        if (SP_DIRECT_POLL && !done && e == NONE && waiting && !local && !(SLAB && in_role))
+            vpoll = sp_ld32(ring + sp_slot(h, P.cap));
         // the shard's tail word, read once for the wave's waiting lanes
         unsigned long long qw = 0;
         if (__any(!done && e == NONE && waiting && !(SLAB && in_role))) {
@@ -814,8 +823,11 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 atomicAdd(&P.ctl[SP_INDONE], 1ull);
             }
         } else if (!done && e == NONE && !local) {   // a ring lane: its ticket's slot
-            // the slot is read only once the tail has passed it (appended; its store may still land)
-            const unsigned v = h < (qw & 0xffffffffull) ? sp_ld32(ring + sp_slot(h, P.cap)) : 0u;
+            // SP_DIRECT_POLL: the slot is polled every iteration, in the same round trip as the tail read
+            // (a slot not yet appended, or appended but not yet stored, reads 0: every slot a sweep uses is
+            // zeroed by its taker, and positions restart at 0 each sweep); otherwise only once the tail has
+            // passed it (appended; its store may still land) -- a second round trip per pick-up
+            const unsigned v = SP_DIRECT_POLL ? vpoll : (h < (qw & 0xffffffffull) ? sp_ld32(ring + sp_slot(h, P.cap)) : 0u);
             if (v) {
                 sp_st32(ring + sp_slot(h, P.cap), 0u);
                 e = SDF_CHK(28, v - 1, P.c_lo, P.c_lo + P.n);

@@ -67,21 +67,22 @@ def _covering(lo, hi, c0, c1, n, d):
     return (xl - c0) // ST_T, (xh - c0) // ST_T
 
 
-def chain_model(ni, nj, nk, nslabs):
+def chain_model(ni, nj, nk, nslabs, nsw=8):
     """tile_sweep_multi's schedule model (sweep_tile.hpp) for all slabs: the critical path of the
     first-pass launch in tile steps.  Estimated starts: +1 hop per upstream tile of the same sweep
-    (across slab boundaries too), + one tile duration after each previous-sweep tile it waits for."""
+    (across slab boundaries too), + one tile duration after each previous-sweep tile it waits for.
+    nsw < 8: the launch holds the first nsw sweeps only (the others run as Jacobi + repair)."""
     A, B = ni - 1, nj - 1
     nJ = (B + ST_T - 1) // ST_T
     kb = [r * nk // nslabs for r in range(nslabs + 1)]
     wc = (A + 2.0 * (ST_T - 1)) / ST_T
     cs, ce, nK = {}, {}, {}
-    for q in range(8):
+    for q in range(nsw):
         for r in range(nslabs):
             cs[q, r], ce[q, r] = _c_range(kb[r], kb[r + 1], nk, DIRS[q][2])
             nK[q, r] = max(0, (ce[q, r] - cs[q, r] + ST_T - 1) // ST_T)
     kv = {}
-    for q in range(8):
+    for q in range(nsw):
         d, dp = DIRS[q], DIRS[(q + 7) % 8]
         for rr in range(nslabs):
             r = rr if d[2] > 0 else nslabs - 1 - rr
