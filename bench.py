@@ -421,6 +421,10 @@ def main():
         # Co-resident slabs: the persistent first-pass grids must fit on the one GPU together
         # (3 tile workgroups per CU), or a waiting slab can hold every CU its upstream slab needs.
         os.environ["SDFGEN_TILE_GRID"] = str(max(32, 3 * 256 // ((world + ndev - 1) // ndev) - 32))
+    if shared and "SDFGEN_SPARSE_WORKERS" not in os.environ:
+        # ... and so must the slabs' repair kernels (each ends only after its upstream neighbour's): the
+        # chip holds 2,048 of their one-wave workgroups (171 VGPRs), the default is 256 per slab
+        os.environ["SDFGEN_SPARSE_WORKERS"] = str(max(32, 1024 // ((world + ndev - 1) // ndev)))
     _hiprt.set_device(dev)
     topo = None
     if world > 1:

@@ -104,8 +104,10 @@ constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup
 #endif
 static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least one ring lane");
 #ifndef SP_DIRECT_POLL
-#define SP_DIRECT_POLL 1   // k_sp_recheck: a waiting ring lane polls its slot in the same round trip as the
-                           // wave's tail read (the tail only decides the shard's drain), not after it
+#define SP_DIRECT_POLL 0   // k_sp_recheck: a waiting ring lane polls its slot in the same round trip as the
+                           // wave's tail read (the tail only decides the shard's drain), not after it.
+                           // Measured neutral (round 5: C3 second pass 2.951-2.962 vs 2.957-2.969 ms,
+                           // C4 12.22-12.28 vs 12.21-12.22 ms, profiles/r05b_ab_directpoll.log): off
 #endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)

@@ -108,7 +108,7 @@ struct StCfg {
     static constexpr bool TWIN = TWIN_;                 // lane L + 32 is the twin of cell lane L
     static constexpr int LPC = LPC_;                    // lanes per cell: lanes LPC x .. LPC x + LPC - 1 are cell x
     static constexpr bool QUAD = LPC_ > 1;              // the lanes-per-cell step (quad or duo lanes): no compaction
-    static constexpr int LPC_SH = LPC_ == 4 ? 2 : (LPC_ == 2 ? 1 : 0);
+    static constexpr int LPC_SH = LPC_ == 8 ? 3 : (LPC_ == 4 ? 2 : (LPC_ == 2 ? 1 : 0));
     static constexpr int WPE = WPE_;
     static constexpr int LEAD = NCW > 1 ? RR - 4 : 0;   // max lead of wave w over wave w+1 (ring hazard)
     static constexpr int THREADS = 64 * (NCW + 1);      // compute waves + helper wave
@@ -116,10 +116,10 @@ struct StCfg {
     static constexpr int HALO0 = RING0 + RR * ST_NCOL;              // 17 streams x RH
     static constexpr int OWN0 = HALO0 + ST_NSTREAM * ST_RH;         // RO slots x 64 columns
     static constexpr int ENTS = OWN0 + ST_RO * ST_NCOL;
-    static_assert(NCW >= 1 && NCW <= 4 && ST_T % NCW == 0, "compute waves must split the tile's c-columns");
+    static_assert(NCW >= 1 && (NCW <= 4 || LPC_ == 8) && ST_T % NCW == 0, "compute waves must split the tile's c-columns");
     static_assert(NCW <= 3 || QUAD, "four compute waves: the quad-lane step only");
     static_assert(!TWIN || CPW == 32, "twin lanes: a compute wave owns 32 cells (lane L + 32 is L's twin)");
-    static_assert(LPC == 1 || LPC == 2 || LPC == 4, "lanes per cell: 1, 2 or 4");
+    static_assert(LPC == 1 || LPC == 2 || LPC == 4 || LPC == 8, "lanes per cell: 1, 2, 4 or 8");
     static_assert(!QUAD || (CPW * LPC == 64 && !TWIN), "lanes per cell: a compute wave owns 64 / LPC cells");
     // Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
     // neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the
@@ -152,8 +152,18 @@ using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, 4>;
 #define ST_DUO_WPE 3
 #endif
 using StCfgDuo = StCfg<2, 8, false, ST_DUO_WPE, 2>;
+// Oct lanes (round 5): 8 compute waves of 8 cells (one c-column each), EIGHT lanes per cell with FIXED
+// roles -- lane 0 reads the cell's own entry, lane 1 + q the entry of upwind neighbour q -- so a step is
+// one batch of LDS reads (no candidate ranking, no select trees: every address is known before any label
+// is), one point-triangle distance per lane, and a first-minimum reduction over the 8 lanes (three DPP
+// moves); the winning lane, which holds the winner's vertices, writes the ring entry back.  Same
+// instructions per cell as the quad tiles, a shorter dependent chain per step.  9 waves per tile.
+#ifndef ST_OCT_WPE
+#define ST_OCT_WPE 4
+#endif
+using StCfgOct = StCfg<8, 8, false, ST_OCT_WPE, 8>;
 
-enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3 };
+enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3, ST_CFG_OCT = 4 };
 // The configuration of a launch with `tiles` tasks per sweep: the quad-lane one while the step
 // latency is what counts, the throughput one once a sweep offers far more tiles than the chip holds
 // at once (768: 3 per CU).  Round 4, first pass, before the quad step's instruction-count work:
@@ -165,7 +175,7 @@ enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3 };
 constexpr long long ST_QUAD_MAX_TILES = 2000;
 inline int st_cfg(long long tiles)
 {
-    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(3, atoi(e)));
+    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(4, atoi(e)));
     return tiles > ST_QUAD_MAX_TILES ? ST_CFG_THR : ST_CFG_QUAD;
 }
 inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
@@ -364,7 +374,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     __shared__ int s_pd[ST_NCW][Cfg::QUAD ? 1 : 14 * ST_CPW + 64];
     // s_hdr: [0] own entries ready for steps < s_hdr[0] (helper), [1 + w] steps completed by
     // compute wave w.
-    __shared__ __attribute__((aligned(16))) int s_hdr[ST_NCW < 4 ? 4 : 8];
+    __shared__ __attribute__((aligned(16))) int s_hdr[ST_NCW < 4 ? 4 : (ST_NCW < 8 ? 8 : 12)];
     // halo entries < s_halo_ready[s] are in LDS; the extra last word is never "not ready"
     // (the stream index of lanes that read no halo stream)
     __shared__ int s_halo_ready[ST_NSTREAM + 1];
@@ -565,6 +575,19 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     for (int q = 0; q < 7; ++q) nb_base[q] = ((nb_base[q] & 0xffff) * 48) | (nb_base[q] & ~0xffff);
                 }
             }
+            // oct lanes: lane qr's fixed entry -- qr = 0 the cell's own (own ring), qr = 1 + q upwind
+            // neighbour q -- as a byte offset o_base + ((((a - o_am) & o_mask) * 48) << o_sh)
+            int o_base = 0, o_sh = 6, o_mask = ST_RO - 1, o_am = 0, o_seen = -1;
+            if constexpr (Cfg::LPC == 8) {
+                const int q = qr - 1, qs = qr > 0 ? q : 0;
+                const int nbq = st_sel7(qs, nb_base[0], nb_base[1], nb_base[2], nb_base[3], nb_base[4], nb_base[5], nb_base[6]);
+                o_base = qr > 0 ? (nbq & 0xffff) : __umul24(ST_OWN0 + col_id, 48);
+                o_sh = qr > 0 ? (nbq >> 16) : 6;
+                o_mask = qr > 0 ? ST_RR - 1 : ST_RO - 1;   // ring and halo slots: RR == RH (NB_PACK)
+                o_am = (qr > 0 && (q & 1) == 0) ? 1 : 0;   // q = 0, 2, 4, 6 read a - 1
+                o_seen = qr > 0 ? st_sel7(qs, P.seen[0], P.seen[1], P.seen[2], P.seen[3], P.seen[4], P.seen[5], P.seen[6]) : -1;
+                static_assert(Cfg::LPC != 8 || (NB_PACK && ST_RR == ST_RH), "oct lanes: packed byte-offset entries");
+            }
             const int hsA = (bl == 0) ? cl : ST_NSTREAM, hsB = (cl == 0) ? ST_T + bl : ST_NSTREAM,
                       hsC = (bl == 0 && cl == 0) ? 2 * ST_T : ST_NSTREAM;
             unsigned polls = 0;
@@ -649,6 +672,75 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 const unsigned long long tc0 = (TRACE && P.trace) ? wall_clock64() : 0ull;
                 const unsigned long long cc0 = (TRACE && P.trace) ? clock64() : 0ull;
                 polls = 0;
+                if constexpr (Cfg::LPC == 8) {
+                    // ---- oct lanes: ONE batch of LDS reads -- lane qr's entry (label + vertices) and the
+                    //      cell's own label and phi -- then lane 1 + q evaluates neighbour q's triangle unless
+                    //      it is none, the cell's own label or already examined (exact skips: sweep_sparse.hpp),
+                    //      a first minimum over the 7 candidates in check order (ties to the lower q: the
+                    //      reference's strict '<' applied in order, cpu_lib/makelevelset3.cpp:94-99, 143-149),
+                    //      then '<' against phi.  The winner lane (lane 0 if nothing wins) writes back. ----
+                    float4 p0 = make_float4(0.f, 0.f, 0.f, 0.f), p1 = p0, p2 = p0;
+                    uint32_t ownw = 0xffffffffu;
+                    float ownphi = 0.f;
+                    if (actx) {
+                        const int e = o_base + (__umul24((a - o_am) & o_mask, 48) << o_sh);
+                        const int eo = __umul24(ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id, 48);
+                        p0 = st_e<true>(s_ent, e, 0);
+                        p1 = st_e<true>(s_ent, e, 1);
+                        p2 = st_e<true>(s_ent, e, 2);
+                        ownw = __float_as_uint(st_e<true>(s_ent, eo, 0).w);
+                        ownphi = st_e<true>(s_ent, eo, 1).w;
+                    }
+                    const uint32_t wq = __float_as_uint(p0.w);
+                    const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
+                    const bool keep = actx && qr > 0 && (wq & LBL_MASK) != LBL_MASK && (wq & LBL_MASK) != (ownw & LBL_MASK) &&
+                                      !(interior && lc_of(wq) <= o_seen);
+                    float key = __builtin_inff();
+                    if (__any(keep)) {
+                        const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(p0), st_xyz(p1), st_xyz(p2), p2.w);
+                        key = (keep && d == d) ? d : __builtin_inff();
+                        if (P.stats) n_evals += (L == 0) ? (unsigned long long)__popcll(__ballot(keep)) : 0ull;
+                    }
+                    // first minimum over the 8 lanes of the cell (keys are never NaN): partner lane^1, lane^2,
+                    // then the other quad (row_half_mirror: lane i <-> 7 - i); the higher lane gives way on ties
+                    int idx = qr;
+                    {
+                        float kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0xB1, 0xf, 0xf, false));
+                        int ip = __builtin_amdgcn_mov_dpp(idx, 0xB1, 0xf, 0xf, false);
+                        bool tk = (kp < key) | ((qr & 1) && kp == key);
+                        key = tk ? kp : key;
+                        idx = tk ? ip : idx;
+                        kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x4E, 0xf, 0xf, false));
+                        ip = __builtin_amdgcn_mov_dpp(idx, 0x4E, 0xf, 0xf, false);
+                        tk = (kp < key) | ((qr & 2) && kp == key);
+                        key = tk ? kp : key;
+                        idx = tk ? ip : idx;
+                        kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(key), 0x141, 0xf, 0xf, false));
+                        ip = __builtin_amdgcn_mov_dpp(idx, 0x141, 0xf, 0xf, false);
+                        tk = (kp < key) | ((qr & 4) && kp == key);
+                        key = tk ? kp : key;
+                        idx = tk ? ip : idx;
+                    }
+                    const bool take = key < ownphi;   // NaN phi: nothing replaces it, as in the reference
+                    if (actx && qr == (take ? idx : 0)) {
+                        const uint32_t w_new = take ? lo_word((int)(wq & LBL_MASK), P.sweep + 1) : ownw;
+                        const float phi_new = take ? key : ownphi;
+                        const int slot = __umul24(ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id, 48);
+                        st_e<true>(s_ent, slot, 0) = make_float4(p0.x, p0.y, p0.z, __uint_as_float(w_new));
+                        st_e<true>(s_ent, slot, 1) = make_float4(p1.x, p1.y, p1.z, phi_new);
+                        st_e<true>(s_ent, slot, 2) = p2;
+                        if (take && ST_DIAG_SPLIT != 1)
+                            P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
+                                ((unsigned long long)__float_as_uint(phi_new) << 32) | w_new;
+                        const unsigned long long gran = st_granule(P.epoch, w_new);
+                        if (bl == ST_T - 1 && J < P.nJ - 1)
+                            __hip_atomic_store(P.hb + ((size_t)J * P.hbC + (c - P.cs)) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                        if (cl == ST_T - 1 && K < P.nK - 1)
+                            __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                        if (SLAB && P.hc_out && c == P.ce - 1)
+                            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                } else {
                 // ---- candidates: the 7 upwind labels minus exact duplicates ----
                 float phi = 0.f;
                 int ct = -1, win = -1;
@@ -1058,6 +1150,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);
                 }
+                }   // LPC != 8
                 if (TRACE && P.trace) {
                     t_comp += wall_clock64() - tc0;
                     c_comp += clock64() - cc0;
@@ -1474,6 +1567,7 @@ inline void st_launch(int cfg, int grid, hipStream_t st, StParams &P, int lead_o
     if (cfg == ST_CFG_THR) st_launch_cfg<StCfgThr, SLAB, TRACE, MULTI>("thr", grid, st, P, lead_override);
     else if (cfg == ST_CFG_QUAD) st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
     else if (cfg == ST_CFG_DUO) st_launch_cfg<StCfgDuo, SLAB, TRACE, MULTI>("duo", grid, st, P, lead_override);
+    else if (cfg == ST_CFG_OCT) st_launch_cfg<StCfgOct, SLAB, TRACE, MULTI>("oct", grid, st, P, lead_override);
     else st_launch_cfg<StCfgLat, SLAB, TRACE, MULTI>("lat", grid, st, P, lead_override);
 }
 

@@ -138,9 +138,12 @@ def test_eight_slabs_in_process_match_reference_digest(name, mode):
     one process -- every slab with both neighbours but the ends, seven slab boundaries per sweep --
     against the reference's SHA-256 of phi.  `slabs`: the slab C-ABI driven per slab (8 streams, one
     hardware queue each); `cabi`: sdfgen_hip_make_level_set3(ngpu=8), the library's own in-process
-    multi-device path, with SDFGEN_DEBUG_SLABS_ONE_DEVICE.  The persistent tile grids are capped
-    (48 workgroups per slab) so that all eight slabs stay co-resident; on 8 GPUs nothing is shared."""
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", SDFGEN_TILE_GRID="48")
+    multi-device path, with SDFGEN_DEBUG_SLABS_ONE_DEVICE.  The persistent grids are capped so that
+    all eight slabs stay co-resident: 48 tile workgroups and 64 repair workgroups per slab (a slab's
+    repair kernel ends only after its upstream neighbour's, so all eight must be resident at once: 8 x
+    the default 256 one-wave repair workgroups at 171 VGPRs are exactly the chip's 2,048 wave slots for
+    them -- a first run without the cap ran into the repair watchdogs).  On 8 GPUs nothing is shared."""
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", SDFGEN_TILE_GRID="48", SDFGEN_SPARSE_WORKERS="64")
     args = ["8", name, "2" if name.startswith("c2") else "1"] + (["--cabi"] if mode == "cabi" else [])
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"), *args],
                        env=env, capture_output=True, text=True, timeout=600)

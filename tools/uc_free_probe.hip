@@ -8,9 +8,10 @@
 //   A  prime:   a block (uncached, or a plain hipMalloc block as the control) carries a producer/consumer
 //               hand-off of tagged 8-byte granules between workgroup pairs on every CU, system scope
 //   F  free:    hipFree(block)
-//   B  reuse:   hipMalloc until a block lands on the freed range (kept: at most 64 tries), zero it with
-//               hipMemsetAsync as st_grow does, then the tile sweep's hand-off form (agent scope) on it,
-//               twice, and a plain fill read back by hipMemcpy
+//   B  reuse:   hipMalloc blocks of 2 .. 128 MiB until one covers the freed range (at most 64 tries; a
+//               first version asking for 2 MiB blocks only never got the range back), zero the block
+//               with hipMemsetAsync as st_grow does, then the tile sweep's hand-off form (agent scope) on
+//               exactly the freed range, twice, and a plain fill read back by hipMemcpy
 // and counts granules a consumer never saw (bounded spins: a lost store ends as a count, not a hang) and
 // words that read back wrong.  Every kernel's spin has an exit every wave reaches.
 //   build: hipcc --offload-arch=gfx950 -O3 -o tools/uc_free_probe tools/uc_free_probe.hip
@@ -71,7 +72,7 @@ __global__ void k_fill(u64 *g, u64 salt)
 
 struct Res {
     unsigned lostA, badA, lostB, badB, lostB2, badB2;
-    size_t fill_bad;
+    size_t fill_bad, off, blk;
     int tries;
     bool reused;
 };
@@ -98,20 +99,32 @@ static Res run(bool uncached, unsigned *d_fail, unsigned ep)
     CHK(hipMemset(a, 0, BYTES));
     handoff(a, ep, true, d_fail, &r.lostA, &r.badA);
     CHK(hipFree(a));
+    // hipMalloc blocks of growing sizes (2 MiB .. 128 MiB, as the tile sweep's halo buffers are) until
+    // one covers the freed range; the hand-off then runs on exactly that range inside it
     std::vector<u64 *> held;
-    u64 *b = nullptr;
+    u64 *b = nullptr, *blk = nullptr;
+    size_t blk_bytes = 0;
     for (r.tries = 1; r.tries <= 64; ++r.tries) {
-        CHK(hipMalloc((void **)&b, BYTES));
-        if (b == a) break;
-        held.push_back(b);
-        b = nullptr;
+        const size_t sz = BYTES << ((r.tries - 1) % 7);
+        u64 *x = nullptr;
+        CHK(hipMalloc((void **)&x, sz));
+        if ((char *)x <= (char *)a && (char *)a + BYTES <= (char *)x + sz) {
+            blk = x;
+            blk_bytes = sz;
+            b = a;   // the freed range, inside the new block
+            break;
+        }
+        held.push_back(x);
     }
     r.reused = b != nullptr;
-    if (!b) {   // the range was not handed out again: test the last block anyway
-        b = held.back();
-        held.pop_back();
+    if (!b) {   // the range was not handed out again: test a fresh block anyway
+        CHK(hipMalloc((void **)&blk, BYTES));
+        blk_bytes = BYTES;
+        b = blk;
     }
-    CHK(hipMemsetAsync(b, 0, BYTES, 0));
+    r.off = (size_t)((char *)b - (char *)blk);
+    r.blk = blk_bytes;
+    CHK(hipMemsetAsync(blk, 0, blk_bytes, 0));
     handoff(b, ep + 1, false, d_fail, &r.lostB, &r.badB);
     handoff(b, ep + 2, false, d_fail, &r.lostB2, &r.badB2);
     hipLaunchKernelGGL(k_fill, dim3(1024), dim3(256), 0, 0, b, (u64)ep);
@@ -120,7 +133,7 @@ static Res run(bool uncached, unsigned *d_fail, unsigned ep)
     std::vector<u64> h(NG);
     CHK(hipMemcpy(h.data(), b, BYTES, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < NG; ++i) r.fill_bad += h[i] != (((u64)ep << 32) ^ i);
-    CHK(hipFree(b));
+    CHK(hipFree(blk));
     for (u64 *p : held) CHK(hipFree(p));
     return r;
 }
@@ -142,10 +155,10 @@ int main(int argc, char **argv)
             ep += 4;
             const unsigned long long bad = (unsigned long long)r.lostB + r.badB + r.lostB2 + r.badB2 + r.fill_bad;
             total_bad += bad != 0;
-            printf("round %d %-9s prime: lost %u bad %u | freed range handed out again: %s (try %d) | reuse hand-off: lost %u "
-                   "bad %u, again: lost %u bad %u | fill read-back wrong words %zu\n",
-                   k, uc ? "uncached" : "plain", r.lostA, r.badA, r.reused ? "yes" : "no", r.tries, r.lostB, r.badB, r.lostB2,
-                   r.badB2, r.fill_bad);
+            printf("round %d %-9s prime: lost %u bad %u | freed range handed out again: %s (try %d, inside a %zu MiB block at "
+                   "offset %zu) | reuse hand-off: lost %u bad %u, again: lost %u bad %u | fill read-back wrong words %zu\n",
+                   k, uc ? "uncached" : "plain", r.lostA, r.badA, r.reused ? "yes" : "no", r.tries, r.blk >> 20, r.off, r.lostB,
+                   r.badB, r.lostB2, r.badB2, r.fill_bad);
             fflush(stdout);
         }
     printf("%s\n", total_bad ? "REPRODUCED: wrong data on a reused range" : "not reproduced: every reuse read back correct");
