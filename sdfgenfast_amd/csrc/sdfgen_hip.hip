@@ -1334,7 +1334,8 @@ int slab_preload_kernels(Err &err)
                        (const void *)k_sweep_tile<StCfgDuo, true, false, false>,
                        (const void *)k_sweep_tile<StCfgDuo, true, false, true>,
                        (const void *)k_sweep_tile<StCfgOct, true, false, false>,
-                       (const void *)k_sweep_tile<StCfgOct, true, false, true>, (const void *)k_sp_jacobi<true>,
+                       (const void *)k_sweep_tile<StCfgOct, true, false, true>,
+                       (const void *)k_sweep_tile<StCfgQfp, true, false, true>, (const void *)k_sp_jacobi<true>,
                        (const void *)k_sp_jlist<true>, (const void *)k_sp_recheck<true>, (const void *)k_sp_slab_wait,
                        (const void *)k_sp_slab_halo, (const void *)k_sp_slab_export};
     for (const void *f : k) {

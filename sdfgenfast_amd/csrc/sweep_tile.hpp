@@ -99,8 +99,9 @@ static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: powe
 
 // Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, the waves
 // per SIMD the register budget must allow, and lanes per cell (4: quad lanes, 2: duo lanes).
-template <int NCW_, int RR_, bool TWIN_, int WPE_, int LPC_ = 1>
+template <int NCW_, int RR_, bool TWIN_, int WPE_, int LPC_ = 1, bool FIX_ = false>
 struct StCfg {
+    static constexpr bool FIX = FIX_;                   // quad lanes with fixed slots (q = r, r + 4) in one packed pass
     static constexpr int NCW = NCW_;                    // compute waves per tile
     static constexpr int CLW = ST_T / NCW;              // c-columns per compute wave
     static constexpr int CPW = ST_T * CLW;              // cells per compute wave
@@ -162,8 +163,18 @@ using StCfgDuo = StCfg<2, 8, false, ST_DUO_WPE, 2>;
 #define ST_OCT_WPE 4
 #endif
 using StCfgOct = StCfg<8, 8, false, ST_OCT_WPE, 8>;
+// Fixed quad lanes (round 5): the quad tiles' geometry (4 compute waves x 16 cells, 4 lanes per cell)
+// with the oct tiles' fixed roles -- lane r of a cell holds upwind neighbour q = r and q = r + 4 (lane 3:
+// q = 3 and the cell's own entry), read in ONE batch of LDS reads, both evaluated in one packed-FP32
+// pass (ptd_wave2); first minima over the quad for q = 0..3 and q = 4..6, the earlier group kept on
+// ties; the lane holding the winner writes back.  No candidate ranking, no select trees, no duplicate
+// test (a duplicate label evaluates to the same distance and loses the tie to the earlier slot).
+#ifndef ST_QFP_WPE
+#define ST_QFP_WPE 4
+#endif
+using StCfgQfp = StCfg<4, 8, false, ST_QFP_WPE, 4, true>;
 
-enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3, ST_CFG_OCT = 4 };
+enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3, ST_CFG_OCT = 4, ST_CFG_QFP = 5 };
 // The configuration of a launch with `tiles` tasks per sweep: the quad-lane one while the step
 // latency is what counts, the throughput one once a sweep offers far more tiles than the chip holds
 // at once (768: 3 per CU).  Round 4, first pass, before the quad step's instruction-count work:
@@ -175,7 +186,7 @@ enum { ST_CFG_LAT = 0, ST_CFG_THR = 1, ST_CFG_QUAD = 2, ST_CFG_DUO = 3, ST_CFG_O
 constexpr long long ST_QUAD_MAX_TILES = 2000;
 inline int st_cfg(long long tiles)
 {
-    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(4, atoi(e)));
+    if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(5, atoi(e)));
     return tiles > ST_QUAD_MAX_TILES ? ST_CFG_THR : ST_CFG_QUAD;
 }
 inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
@@ -588,6 +599,23 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 o_seen = qr > 0 ? st_sel7(qs, P.seen[0], P.seen[1], P.seen[2], P.seen[3], P.seen[4], P.seen[5], P.seen[6]) : -1;
                 static_assert(Cfg::LPC != 8 || (NB_PACK && ST_RR == ST_RH), "oct lanes: packed byte-offset entries");
             }
+            // fixed quad lanes: slot A = neighbour q = qr (o_*), slot B = neighbour q = qr + 4, or (qr = 3) the own entry
+            int f_base = 0, f_sh = 6, f_mask = ST_RO - 1, f_am = 0, f_seen = -1;
+            if constexpr (Cfg::FIX) {
+                const int nba = st_sel4(qr, nb_base[0], nb_base[1], nb_base[2], nb_base[3]);
+                o_base = nba & 0xffff;
+                o_sh = nba >> 16;
+                o_mask = ST_RR - 1;
+                o_am = (qr & 1) ? 0 : 1;   // q = 0, 2 read a - 1
+                o_seen = st_sel4(qr, P.seen[0], P.seen[1], P.seen[2], P.seen[3]);
+                const int nbb = st_sel4(qr, nb_base[4], nb_base[5], nb_base[6], nb_base[6]);
+                f_base = qr < 3 ? (nbb & 0xffff) : __umul24(ST_OWN0 + col_id, 48);
+                f_sh = qr < 3 ? (nbb >> 16) : 6;
+                f_mask = qr < 3 ? ST_RR - 1 : ST_RO - 1;
+                f_am = (qr == 0 || qr == 2) ? 1 : 0;   // q = 4, 6 read a - 1; q = 5 and the own entry read a
+                f_seen = qr < 3 ? st_sel4(qr, P.seen[4], P.seen[5], P.seen[6], P.seen[6]) : -1;
+                static_assert(!Cfg::FIX || (Cfg::LPC == 4 && NB_PACK && ST_RR == ST_RH), "fixed quad lanes: packed byte-offset entries");
+            }
             const int hsA = (bl == 0) ? cl : ST_NSTREAM, hsB = (cl == 0) ? ST_T + bl : ST_NSTREAM,
                       hsC = (bl == 0 && cl == 0) ? 2 * ST_T : ST_NSTREAM;
             unsigned polls = 0;
@@ -729,6 +757,97 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         st_e<true>(s_ent, slot, 0) = make_float4(p0.x, p0.y, p0.z, __uint_as_float(w_new));
                         st_e<true>(s_ent, slot, 1) = make_float4(p1.x, p1.y, p1.z, phi_new);
                         st_e<true>(s_ent, slot, 2) = p2;
+                        if (take && ST_DIAG_SPLIT != 1)
+                            P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
+                                ((unsigned long long)__float_as_uint(phi_new) << 32) | w_new;
+                        const unsigned long long gran = st_granule(P.epoch, w_new);
+                        if (bl == ST_T - 1 && J < P.nJ - 1)
+                            __hip_atomic_store(P.hb + ((size_t)J * P.hbC + (c - P.cs)) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                        if (cl == ST_T - 1 && K < P.nK - 1)
+                            __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                        if (SLAB && P.hc_out && c == P.ce - 1)
+                            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    }
+                } else if constexpr (Cfg::FIX) {
+                    // ---- fixed quad lanes: one batch of LDS reads (lane qr: neighbours qr and qr + 4, lane 3 the
+                    //      own entry as its second slot; every lane the own label and phi), one packed pass
+                    //      (ptd_wave2), first minima over the quad for q = 0..3 and q = 4..6 (ties to the lower
+                    //      q; the q = 0..3 group wins ties against q = 4..6), then '<' against phi -- the
+                    //      reference's strict '<' in check order (cpu_lib/makelevelset3.cpp:94-99, 143-149) ----
+                    float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, b0_ = a0, b1_ = a0, b2_ = a0;
+                    uint32_t ownw = 0xffffffffu;
+                    float ownphi = 0.f;
+                    const int ea = o_base + (__umul24((a - o_am) & o_mask, 48) << o_sh);
+                    const int eb = f_base + (__umul24((a - f_am) & f_mask, 48) << f_sh);
+                    if (actx) {
+                        const int eo = __umul24(ST_OWN0 + (a & (ST_RO - 1)) * ST_NCOL + col_id, 48);
+                        a0 = st_e<true>(s_ent, ea, 0);
+                        a1 = st_e<true>(s_ent, ea, 1);
+                        a2 = st_e<true>(s_ent, ea, 2);
+                        b0_ = st_e<true>(s_ent, eb, 0);
+                        b1_ = st_e<true>(s_ent, eb, 1);
+                        b2_ = st_e<true>(s_ent, eb, 2);
+                        ownw = __float_as_uint(st_e<true>(s_ent, eo, 0).w);
+                        ownphi = st_e<true>(s_ent, eo, 1).w;
+                    }
+                    const uint32_t wa = __float_as_uint(a0.w), wb = __float_as_uint(b0_.w);
+                    const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
+                    const uint32_t own_raw = ownw & LBL_MASK;
+                    const bool keep_a = actx && (wa & LBL_MASK) != LBL_MASK && (wa & LBL_MASK) != own_raw &&
+                                        !(interior && lc_of(wa) <= o_seen);
+                    const bool keep_b = actx && qr < 3 && (wb & LBL_MASK) != LBL_MASK && (wb & LBL_MASK) != own_raw &&
+                                        !(interior && lc_of(wb) <= f_seen);
+                    float ka = __builtin_inff(), kb = __builtin_inff();
+                    if (__any(keep_a | keep_b)) {
+                        const f3 gx = st_gx(P, a, b, c);
+                        float da, db;
+                        ptd_wave2(gx, st_xyz(a0), st_xyz(a1), st_xyz(a2), a2.w, gx, st_xyz(b0_), st_xyz(b1_), st_xyz(b2_), b2_.w,
+                                  da, db);
+                        ka = (keep_a && da == da) ? da : __builtin_inff();
+                        kb = (keep_b && db == db) ? db : __builtin_inff();
+                        if (P.stats) n_evals += (L == 0) ? (unsigned long long)(__popcll(__ballot(keep_a)) + __popcll(__ballot(keep_b))) : 0ull;
+                    }
+                    // first minima over the quad (keys are never NaN), the higher lane giving way on ties
+                    int ia = qr, ib = qr;
+                    {
+                        const bool q_odd = qr & 1, q_hi = qr & 2;
+                        float kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(ka), 0xB1, 0xf, 0xf, false));
+                        int ip = __builtin_amdgcn_mov_dpp(ia, 0xB1, 0xf, 0xf, false);
+                        bool tk = (kp < ka) | (q_odd & (kp == ka));
+                        ka = tk ? kp : ka;
+                        ia = tk ? ip : ia;
+                        float kq = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(kb), 0xB1, 0xf, 0xf, false));
+                        int iq = __builtin_amdgcn_mov_dpp(ib, 0xB1, 0xf, 0xf, false);
+                        bool tq = (kq < kb) | (q_odd & (kq == kb));
+                        kb = tq ? kq : kb;
+                        ib = tq ? iq : ib;
+                        kp = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(ka), 0x4E, 0xf, 0xf, false));
+                        ip = __builtin_amdgcn_mov_dpp(ia, 0x4E, 0xf, 0xf, false);
+                        tk = (kp < ka) | (q_hi & (kp == ka));
+                        ka = tk ? kp : ka;
+                        ia = tk ? ip : ia;
+                        kq = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(kb), 0x4E, 0xf, 0xf, false));
+                        iq = __builtin_amdgcn_mov_dpp(ib, 0x4E, 0xf, 0xf, false);
+                        tq = (kq < kb) | (q_hi & (kq == kb));
+                        kb = tq ? kq : kb;
+                        ib = tq ? iq : ib;
+                    }
+                    const bool use_b = kb < ka;   // q = 4..6 strictly closer than the best of q = 0..3
+                    const float key = use_b ? kb : ka;
+                    const int widx = use_b ? ib : ia;
+                    const bool take = key < ownphi;   // NaN phi: nothing replaces it, as in the reference
+                    // writer: the winner's lane (its slot A or B), else lane 3 (the own entry in its slot B)
+                    if (actx && qr == (take ? widx : 3)) {
+                        // the winner's entry read back (holding both slots' vertices through the packed
+                        // pass took the register allocator past its limits)
+                        const int src = (!take || use_b) ? eb : ea;
+                        const float4 w0 = st_e<true>(s_ent, src, 0), w1 = st_e<true>(s_ent, src, 1), w2 = st_e<true>(s_ent, src, 2);
+                        const uint32_t w_new = take ? lo_word((int)(__float_as_uint(w0.w) & LBL_MASK), P.sweep + 1) : ownw;
+                        const float phi_new = take ? key : ownphi;
+                        const int slot = __umul24(ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id, 48);
+                        st_e<true>(s_ent, slot, 0) = make_float4(w0.x, w0.y, w0.z, __uint_as_float(w_new));
+                        st_e<true>(s_ent, slot, 1) = make_float4(w1.x, w1.y, w1.z, phi_new);
+                        st_e<true>(s_ent, slot, 2) = w2;
                         if (take && ST_DIAG_SPLIT != 1)
                             P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
                                 ((unsigned long long)__float_as_uint(phi_new) << 32) | w_new;
@@ -1434,6 +1553,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 // ---------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------
+
 struct TileSweepWorkspace {
     unsigned long long *hb = nullptr, *hc = nullptr, *stats = nullptr, *trace = nullptr;
     size_t cap_trace = 0;
@@ -1568,6 +1688,12 @@ inline void st_launch(int cfg, int grid, hipStream_t st, StParams &P, int lead_o
     else if (cfg == ST_CFG_QUAD) st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
     else if (cfg == ST_CFG_DUO) st_launch_cfg<StCfgDuo, SLAB, TRACE, MULTI>("duo", grid, st, P, lead_override);
     else if (cfg == ST_CFG_OCT) st_launch_cfg<StCfgOct, SLAB, TRACE, MULTI>("oct", grid, st, P, lead_override);
+    else if (cfg == ST_CFG_QFP) {
+        // (the per-sweep launch of the fixed quad lanes crashed hipcc 7.2's greedy register allocator:
+        // the quad tiles serve it)
+        if constexpr (MULTI) st_launch_cfg<StCfgQfp, SLAB, TRACE, MULTI>("qfp", grid, st, P, lead_override);
+        else st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
+    }
     else st_launch_cfg<StCfgLat, SLAB, TRACE, MULTI>("lat", grid, st, P, lead_override);
 }
 

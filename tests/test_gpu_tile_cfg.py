@@ -16,10 +16,10 @@ from oracle import oracle as O
 from sdfgenfast_amd import _lib, meshgen
 
 pytestmark = pytest.mark.gpu
-CFGS = [0, 1, 2, 3, 4]
+CFGS = [0, 1, 2, 3, 4, 5]
 
 
-@pytest.fixture(params=CFGS, ids=["lat", "thr", "quad", "duo", "oct"])
+@pytest.fixture(params=CFGS, ids=["lat", "thr", "quad", "duo", "oct", "qfp"])
 def cfg(request, monkeypatch):
     monkeypatch.setenv("SDFGEN_TILE_CFG", str(request.param))
     return request.param

@@ -3,9 +3,12 @@
 check against the default split.
     python tools/sparse_from.py [WORKLOAD] [FROM ...]"""
 import hashlib
+import json
 import os
 import sys
 import time
+
+os.environ.setdefault("SDFGEN_SWEEP_EVENTS", "1")   # per-sweep times of the second-pass sweeps (before the first call)
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
@@ -28,3 +31,7 @@ for f in froms:
     print(f"from {f}: total {np.median(ts[2:]):.3f} ms (min {min(ts[2:]):.3f})  sweep {p['sweep_ms']:.3f}  rechecks {p['sparse_rechecks']} claims {p['sparse_claims']}  "
           f"digest {dig} {'OK' if dig == ref else 'MISMATCH'}", flush=True)
     print("   per sweep ms:", " ".join(f"{x:.3f}" for x in p["sweep_launch_ms"]), flush=True)
+    print("JSON " + json.dumps({"workload": name, "from": f, "total_ms": float(np.median(ts[2:])), "sweep_ms": p["sweep_ms"],
+                                "sweep_launch_ms": [round(x, 4) for x in p["sweep_launch_ms"]],
+                                "rechecks": p["sparse_rechecks"], "claims": p["sparse_claims"], "tile_cfg": p["tile_cfg"],
+                                "digest_ok": dig == ref}), flush=True)
