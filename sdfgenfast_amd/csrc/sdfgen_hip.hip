@@ -743,8 +743,9 @@ const int SWEEP_DIRS[8][3] = {{+1, +1, +1}, {-1, -1, -1}, {+1, +1, -1}, {-1, -1,
                               {+1, -1, +1}, {-1, +1, -1}, {+1, -1, -1}, {-1, +1, +1}};
 
 // Status words of one call (run_pipeline): [0] prep error flag, [1] tile sweep error bits, [2] band
-// evaluations, [3, 19) tile sweep statistics, [19, 19 + SP_NCTL) the sparse sweeps' control words.
-constexpr int STATUS_N = 19 + SP_NCTL;
+// evaluations, [3, 3 + ST_NSTATS) tile sweep statistics, then SP_NCTL sparse sweep control words.
+constexpr int STATUS_SP = 3 + ST_NSTATS;
+constexpr int STATUS_N = STATUS_SP + SP_NCTL;
 __global__ void k_status(unsigned long long *__restrict__ out, const int *flag, const int *wf_err,
                          const unsigned long long *evals, const unsigned long long *wf_stats,
                          const unsigned long long *sp_ctl)
@@ -754,8 +755,8 @@ __global__ void k_status(unsigned long long *__restrict__ out, const int *flag, 
         if (t == 0) v = (unsigned)*flag;
         else if (t == 1) v = wf_err ? (unsigned)*wf_err : 0u;
         else if (t == 2) v = *evals;
-        else if (t < 19) v = wf_stats ? wf_stats[t - 3] : 0ull;
-        else v = sp_ctl ? sp_ctl[t - 19] : 0ull;
+        else if (t < STATUS_SP) v = wf_stats ? wf_stats[t - 3] : 0ull;
+        else v = sp_ctl ? sp_ctl[t - STATUS_SP] : 0ull;
         out[t] = v;
     }
 }
@@ -934,7 +935,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         ws->wf.grid_override = gr ? atoi(gr) : 0;
         const char *ld = getenv("SDFGEN_TILE_LEAD");      // diagnostics: inter-wave lead
         ws->wf.lead_override = ld ? atoi(ld) : -1;
-        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, 128, st));
+        if (ws->wf.count && ws->wf.stats) HIPCHK(hipMemsetAsync(ws->wf.stats, 0, ST_NSTATS * sizeof(u64), st));
     }
     const char *nsw_env = getenv("SDFGEN_DEBUG_NSWEEPS");   // diagnostics: stop after n sweeps
     const int nsweeps = nsw_env ? atoi(nsw_env) : 16;
@@ -1049,7 +1050,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     HIPCHK(hipMemcpyAsync(stv, ws->status, sizeof(stv), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const int flag = (int)stv[0], wf_err = (int)stv[1];
-    const unsigned long long evals = stv[2], *wf_stats = stv + 3, *sp_ctl = stv + 19;
+    const unsigned long long evals = stv[2], *wf_stats = stv + 3, *sp_ctl = stv + STATUS_SP;
     HIPCHK(hipGetLastError());
     if ((rc = check_oob(err, "make_level_set3"))) return rc;
 
@@ -1092,6 +1093,10 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         fprintf(stderr, "step profile: failed polls %.0f per wave-step: own data not landed %.3f, wave w-1 behind %.3f, "
                         "wave w+1 ring space %.3f, halo %.3f (a poll can fail on several)\n", wf_stats[1] / steps,
                 wf_stats[3] / steps, wf_stats[14] / steps, (wf_stats[15] & 0xffffffffull) / steps, (wf_stats[15] >> 32) / steps);
+        fprintf(stderr, "step profile: helper %.0f iterations that landed data, %.0f cycles each, %.2f own steps and %.2f halo "
+                        "entries per iteration; %.0f idle polls\n", (double)wf_stats[16],
+                wf_stats[17] / std::max(1.0, (double)wf_stats[16]), wf_stats[18] / std::max(1.0, (double)wf_stats[16]),
+                wf_stats[19] / std::max(1.0, (double)wf_stats[16]), (double)wf_stats[2]);
     }
 #endif
     p.sweep_evals = wf_stats[0];

@@ -192,6 +192,7 @@ inline int st_cfg(long long tiles)
 inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
 
 constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
+constexpr int ST_NSTATS = 24;                 // statistics words (StParams::stats): counts, step and helper profiles
 
 // Entry layout in LDS: [3e] = (x1, w), [3e+1] = (x2, phi -- own entries only), [3e+2] = x3,
 // where w is the cell's low word (label and the sweep that set it: geom.hpp lo_word).
@@ -723,6 +724,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     const bool interior = a <= P.A - 2 && b <= P.B - 2 && c <= P.C - 2;
                     const bool keep = actx && qr > 0 && (wq & LBL_MASK) != LBL_MASK && (wq & LBL_MASK) != (ownw & LBL_MASK) &&
                                       !(interior && lc_of(wq) <= o_seen);
+#ifdef ST_STEP_PROF
+                    {
+                        const unsigned long long t_ = clock64();
+                        sp_c[1] += t_ - sp_t;
+                        sp_t = t_;
+                        ++sp_n[__any(keep) ? 1 : 0];
+                    }
+#endif
                     float key = __builtin_inff();
                     if (__any(keep)) {
                         const float d = ptd_wave(st_gx(P, a, b, c), st_xyz(p0), st_xyz(p1), st_xyz(p2), p2.w);
@@ -749,6 +758,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         key = tk ? kp : key;
                         idx = tk ? ip : idx;
                     }
+#ifdef ST_STEP_PROF
+                    { const unsigned long long t_ = clock64(); sp_c[2] += t_ - sp_t; sp_ev[0] += t_ - sp_t; sp_t = t_; }
+#endif
                     const bool take = key < ownphi;   // NaN phi: nothing replaces it, as in the reference
                     if (actx && qr == (take ? idx : 0)) {
                         const uint32_t w_new = take ? lo_word((int)(wq & LBL_MASK), P.sweep + 1) : ownw;
@@ -797,6 +809,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                                         !(interior && lc_of(wa) <= o_seen);
                     const bool keep_b = actx && qr < 3 && (wb & LBL_MASK) != LBL_MASK && (wb & LBL_MASK) != own_raw &&
                                         !(interior && lc_of(wb) <= f_seen);
+#ifdef ST_STEP_PROF
+                    {
+                        const unsigned long long t_ = clock64();
+                        sp_c[1] += t_ - sp_t;
+                        sp_t = t_;
+                        ++sp_n[__any(keep_a | keep_b) ? (__any(keep_b) ? 2 : 1) : 0];
+                    }
+#endif
                     float ka = __builtin_inff(), kb = __builtin_inff();
                     if (__any(keep_a | keep_b)) {
                         const f3 gx = st_gx(P, a, b, c);
@@ -832,6 +852,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         kb = tq ? kq : kb;
                         ib = tq ? iq : ib;
                     }
+#ifdef ST_STEP_PROF
+                    { const unsigned long long t_ = clock64(); sp_c[2] += t_ - sp_t; sp_ev[0] += t_ - sp_t; sp_t = t_; }
+#endif
                     const bool use_b = kb < ka;   // q = 4..6 strictly closer than the best of q = 0..3
                     const float key = use_b ? kb : ka;
                     const int widx = use_b ? ib : ia;
@@ -1361,6 +1384,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             static_assert(ST_G == 4 || ST_G == 2, "helper pipeline is written out for 2- or 4-element batches");
             unsigned idle = 0;
             unsigned long long t_idle = 0;   // Z-slab: wall ticks this helper spent backing off (TM_*)
+#ifdef ST_STEP_PROF   // helper iterations that landed data: count, cycles (since the previous one), own steps, halo lanes
+            unsigned long long hp_n = 0, hp_cyc = 0, hp_own = 0, hp_halo = 0, hp_t0 = 0;
+#endif
             bool tr_halo = false, tr_own = false;   // TRACE + MULTI: first landings recorded
             for (;;) {
                 // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
@@ -1508,6 +1534,18 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     tr_own |= o_now;
                 }
                 const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
+#ifdef ST_STEP_PROF
+                if (P.stats && __any(moved)) {
+                    const unsigned long long t_ = clock64();
+                    if (hp_t0) {
+                        hp_n += 1;
+                        hp_cyc += t_ - hp_t0;
+                        hp_own += (unsigned long long)gA;
+                        hp_halo += (unsigned long long)__popcll(__ballot(hp > 0)) ;
+                    }
+                    hp_t0 = t_;
+                }
+#endif
                 fA = fB; gA = gB; hA = hB; hcA = hcB;
                 c0 = n0; c1 = n1; c2 = n2; c3 = n3;
                 q0 = m0; q1 = m1; q2 = m2; q3 = m3;
@@ -1529,6 +1567,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     if (SLAB && P.tm) t_idle += wall_clock64() - ts;
                 }
             }
+#ifdef ST_STEP_PROF
+            if (P.stats && L == 0) {
+                atomicAdd(P.stats + 16, hp_n);
+                atomicAdd(P.stats + 17, hp_cyc);
+                atomicAdd(P.stats + 18, hp_own);
+                atomicAdd(P.stats + 19, hp_halo);
+            }
+#endif
             if (SLAB && P.tm && L == 0) {   // where the slab boundary's tiles wait for the upstream GPU
                 atomicAdd(P.tm + (inbox ? TM_INBOX_IDLE : TM_OTHER_IDLE), t_idle);
                 atomicAdd(P.tm + (inbox ? TM_INBOX_TASKS : TM_OTHER_TASKS), 1ull);
@@ -1633,7 +1679,7 @@ inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int
     if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A, st)) return -5;
     if (!W.ctrl) {
         if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return -5;
-        if (hipMalloc((void **)&W.stats, 16 * sizeof(unsigned long long)) != hipSuccess) return -5;
+        if (hipMalloc((void **)&W.stats, ST_NSTATS * sizeof(unsigned long long)) != hipSuccess) return -5;
         if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return -4;
     }
     int ti = (W.task_nJ[0] == nJ && W.task_nK[0] == nK) ? 0 : (W.task_nJ[1] == nJ && W.task_nK[1] == nK) ? 1 : -1;
@@ -1878,7 +1924,7 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc, st)) return fail(-5, "halo buffer allocation failed");
     if (!W.ctrl) {
         if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
-        if (hipMalloc((void **)&W.stats, 16 * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
+        if (hipMalloc((void **)&W.stats, ST_NSTATS * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
         if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return fail(-4, "memset");
     }
     int ntasks = 0;
