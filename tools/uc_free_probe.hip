@@ -90,7 +90,7 @@ static void handoff(u64 *g, unsigned epoch, bool system, unsigned *d_fail, unsig
     *bad = h[1];
 }
 
-static Res run(bool uncached, unsigned *d_fail, unsigned ep)
+static Res run(bool uncached, bool adjacent, unsigned *d_fail, unsigned ep)
 {
     Res r{};
     u64 *a = nullptr;
@@ -98,20 +98,28 @@ static Res run(bool uncached, unsigned *d_fail, unsigned ep)
     else CHK(hipMalloc((void **)&a, BYTES));
     CHK(hipMemset(a, 0, BYTES));
     handoff(a, ep, true, d_fail, &r.lostA, &r.badA);
+    // the round-4 failure freed the comm block together with the session's other buffers, and the next
+    // call's 4.4 MB halo buffer started exactly at the block's address: free a neighbour block as well
+    u64 *nb = nullptr;
+    if (adjacent) CHK(hipMalloc((void **)&nb, 8 * BYTES));
     CHK(hipFree(a));
+    if (nb) CHK(hipFree(nb));
     // hipMalloc blocks of growing sizes (2 MiB .. 128 MiB, as the tile sweep's halo buffers are) until
     // one covers the freed range; the hand-off then runs on exactly that range inside it
     std::vector<u64 *> held;
     u64 *b = nullptr, *blk = nullptr;
     size_t blk_bytes = 0;
     for (r.tries = 1; r.tries <= 64; ++r.tries) {
-        const size_t sz = BYTES << ((r.tries - 1) % 7);
+        // 2 .. 128 MiB, and sizes that straddle the block (the failing halo buffer was 4.4 MB)
+        const size_t sz = (r.tries % 2) ? (BYTES << ((r.tries / 2) % 7)) : (BYTES + (BYTES / 5) * (size_t)(r.tries % 23));
         u64 *x = nullptr;
         CHK(hipMalloc((void **)&x, sz));
-        if ((char *)x <= (char *)a && (char *)a + BYTES <= (char *)x + sz) {
+        if ((char *)x < (char *)a + BYTES && (char *)a < (char *)x + sz) {   // overlaps the freed range
             blk = x;
             blk_bytes = sz;
-            b = a;   // the freed range, inside the new block
+            // the part of the freed range inside the new block (at least one granule pair's chunk)
+            b = (char *)a >= (char *)x ? a : x;
+            if ((size_t)((char *)x + sz - (char *)b) < BYTES) b = (u64 *)((char *)x + sz - BYTES);
             break;
         }
         held.push_back(x);
@@ -150,14 +158,16 @@ int main(int argc, char **argv)
     unsigned ep = 1;
     int total_bad = 0;
     for (int k = 0; k < rounds; ++k)
-        for (int uc = 1; uc >= 0; --uc) {
-            const Res r = run(uc != 0, d_fail, ep);
+        for (int v = 3; v >= 0; --v) {
+            const int uc = v & 1;
+            const bool adj = v & 2;
+            const Res r = run(uc != 0, adj, d_fail, ep);
             ep += 4;
             const unsigned long long bad = (unsigned long long)r.lostB + r.badB + r.lostB2 + r.badB2 + r.fill_bad;
             total_bad += bad != 0;
-            printf("round %d %-9s prime: lost %u bad %u | freed range handed out again: %s (try %d, inside a %zu MiB block at "
+            printf("round %d %-9s %s prime: lost %u bad %u | freed range handed out again: %s (try %d, inside a %zu MiB block at "
                    "offset %zu) | reuse hand-off: lost %u bad %u, again: lost %u bad %u | fill read-back wrong words %zu\n",
-                   k, uc ? "uncached" : "plain", r.lostA, r.badA, r.reused ? "yes" : "no", r.tries, r.blk >> 20, r.off, r.lostB,
+                   k, uc ? "uncached" : "plain", adj ? "+neighbour freed" : "alone          ", r.lostA, r.badA, r.reused ? "yes" : "no", r.tries, r.blk >> 20, r.off, r.lostB,
                    r.badB, r.lostB2, r.badB2, r.fill_bad);
             fflush(stdout);
         }
