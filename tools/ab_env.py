@@ -1,4 +1,5 @@
-"""A/B by environment: python tools/ab_env.py WORKLOAD 'VAR=a' 'VAR=b' ... (each in a subprocess, interleaved)."""
+"""A/B by environment: python tools/ab_env.py WORKLOAD 'VAR=a' 'VAR=b' ... (each in a subprocess, interleaved;
+several variables in one configuration joined by ',' or '+', the latter for tools/session.sh's comma lists)."""
 import json, os, subprocess, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 wl, cfgs = sys.argv[1], sys.argv[2:]
@@ -22,7 +23,7 @@ print(json.dumps({k: best[k] for k in ("total_ms", "band_ms", "sweep_ms", "spars
 for rnd in range(2):
     for cfg in cfgs:
         env = dict(os.environ)
-        for kv in cfg.split(","):
+        for kv in cfg.replace("+", ",").split(","):
             if "=" in kv:
                 k, v = kv.split("=", 1)
                 env[k] = v

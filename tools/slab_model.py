@@ -37,6 +37,12 @@ INPUTS = {
         "t_repair_per_sweep": 0.62,    # repair_ms per sweep, 2-slab rehearsal (r03c_n2 zslab_c4), median
         "t_first_work": 39.882,        # throughput-bound at one GPU: the launch itself
         "longest_chain": 172,          # not measured at C4: 2 x C3's (chains scale with the grid edge)
+        # round 5, one MI355X (profiles/r05d_sparse_from_c4.log, SDFGEN_SPARSE_FROM=k, per-sweep events): the
+        # first pass's last sweeps as Jacobi + repair instead of inside the tile launch -- the tile launch of the
+        # first k sweeps and each later first-pass sweep's own time
+        "sparse_from": {8: {"tile": 42.003, "sparse_first": []},
+                        7: {"tile": 36.051, "sparse_first": [35.897]},
+                        6: {"tile": 32.296, "sparse_first": [30.297, 37.807]}},
     },
 }
 S_ISO_US = 1.1649    # isolated tile step, quad-lane tiles (bench r04v latency probe, 1024x9x9 grid)
@@ -142,12 +148,47 @@ def predict(name, inp, ns=(1, 2, 4, 8)):
             "h_x_us": H_X_US, "rows": rows}
 
 
+def predict_schedules(name, inp, ns=(1, 2, 4, 8)):
+    """an N-dependent split of the first pass -- its first k sweeps in the tile launch,
+    sweeps k..7 as Jacobi + repair -- priced per N.  The tile part scales like the default's first pass
+    (chain of the k-sweep task graph, work / N, crowding); a repair sweep is priced OPTIMISTICALLY at its
+    one-GPU time / N plus the neighbour handshakes (its chains do not really shrink with N),
+    so a split that loses here loses on hardware too.  Only the first-pass time changes; returns rows of
+    (N, k, first-pass ms, total ms, efficiency vs the default 1-GPU run)."""
+    sf = inp.get("sparse_from")
+    if not sf:
+        return []
+    ni, nj, nk = inp["dims"]
+    base = predict(name, inp, ns)["rows"]
+    t1 = base[0]["total_ms"]
+    rows = []
+    for n, b in zip(ns, base):
+        for k in sorted(sf, reverse=True):
+            d = sf[k]
+            c1 = chain_model(ni, nj, nk, 1, k)
+            chain1 = c1 * S_ISO_US * 1e-3
+            work1 = d["tile"] if inp["t_first_work"] == inp["t_first"] else inp["t_first_work"] * k / 8
+            crowd = d["tile"] / max(chain1, work1)
+            cn = chain_model(ni, nj, nk, n, k) if n > 1 else c1
+            chain = cn * S_ISO_US * 1e-3 + k * (n - 1) * H_X_US * 1e-3
+            tile = max(chain, work1 / n) * (1.0 + (crowd - 1.0) / n)
+            rep = sum(t / n + (2 * H_FLAG_US + (n - 1) * H_X_US) * 1e-3 * (n > 1) for t in d["sparse_first"])
+            first = tile + rep
+            total = b["total_ms"] - b["first_ms"] + first
+            rows.append({"n": n, "tile_sweeps": k, "first_ms": round(first, 3), "tile_ms": round(tile, 3),
+                         "repair_sweeps_ms": round(rep, 3), "total_ms": round(total, 3),
+                         "efficiency": round(t1 / (n * total), 3)})
+    return rows
+
+
 def main():
     for name, inp in INPUTS.items():
         res = predict(name, inp)
         print(json.dumps({k: v for k, v in res.items() if k != "rows"}))
         for r in res["rows"]:
             print("  ", json.dumps(r))
+        for r in predict_schedules(name, inp):
+            print("   schedule", json.dumps(r))
 
 
 if __name__ == "__main__":
