@@ -156,7 +156,10 @@ typedef struct sdfgen_hip_profile {
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
 
-/* Free cached device workspaces (they are grow-only between calls). */
+/* Free cached device workspaces (they are grow-only between calls).  With no slab session alive it
+ * also closes the HIP IPC mappings of neighbour slabs' communication blocks; the process's own pool of
+ * uncached communication blocks is kept (power-of-two size classes from 2 MiB, reused by later
+ * sessions). */
 int sdfgen_hip_release(void);
 
 /* ---------------------------------------------------------------------------

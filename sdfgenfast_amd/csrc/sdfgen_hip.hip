@@ -1259,6 +1259,12 @@ std::vector<CommBlock> g_comm;
 
 int comm_acquire(int device, size_t bytes, char **out, Err &err)
 {
+    // power-of-two size classes from 2 MiB: the pool never shrinks, so its growth is bounded by the
+    // concurrently live sessions per class -- a caller cycling through many plane sizes reuses blocks
+    // instead of adding one per size
+    size_t cls = (size_t)2 << 20;
+    while (cls < bytes) cls <<= 1;
+    bytes = cls;
     std::lock_guard<std::mutex> lk(g_comm_mu);
     CommBlock *best = nullptr;
     for (CommBlock &b : g_comm)
@@ -1298,12 +1304,37 @@ int comm_export(char *p, hipIpcMemHandle_t *h, Err &err)
     return err.set(SDFGEN_HIP_ERUNTIME, "slab communication block not found");
 }
 
+// Imported neighbour blocks stay mapped for the life of the process, like the pool: closing a mapping
+// would hand its virtual range back to this process's allocator, the situation the pool avoids.  Growth
+// bound: one mapping per distinct exported block a peer ever showed us (a peer's pool reuses blocks, so
+// long-lived peer processes add none after their first sessions).  Keyed by the handle bytes: a handle
+// is only ever reused by the exporting process for the same block (hipIpcGetMemHandle of a live
+// allocation), and a peer that exited and a new one whose handle bytes collide would map a stale block --
+// callers that replace peer processes call sdfgen_hip_release in the survivors between jobs: with no slab
+// session alive it closes every imported mapping (comm_close_imports).
 struct CommImport {
     int device;
     hipIpcMemHandle_t handle;
     void *p;
 };
 std::vector<CommImport> g_comm_imports;
+int g_live_slabs = 0;   // slab sessions alive in this process (under g_comm_mu)
+
+// Close every imported neighbour mapping once no slab session of this process is alive.  Returns the
+// number closed (0 while a session is alive).
+int comm_close_imports()
+{
+    std::lock_guard<std::mutex> lk(g_comm_mu);
+    if (g_live_slabs > 0) return 0;
+    int n = 0;
+    for (const CommImport &m : g_comm_imports) {
+        (void)hipSetDevice(m.device);
+        if (hipIpcCloseMemHandle(m.p) == hipSuccess) ++n;
+    }
+    (void)hipGetLastError();
+    g_comm_imports.clear();
+    return n;
+}
 
 int comm_import(int device, const hipIpcMemHandle_t &h, void **out, Err &err)
 {
@@ -1374,6 +1405,10 @@ int slab_alloc(SlabSession *S, Err &err)
     // wrote, mid-kernel.  Whole 2 MiB: a dedicated allocation that IPC maps as is.
     S->cl.init(plane);
     if (int rc = comm_acquire(S->device, S->cl.bytes, &S->comm, err)) return rc;
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        ++g_live_slabs;
+    }
     HIPCHK(hipMemset(S->comm, 0, S->cl.bytes));   // epoch 0 is never published, flags start at 0
     HIPCHK(hipDeviceSynchronize());
     return 0;
@@ -1385,7 +1420,11 @@ void slab_free(SlabSession *S)
     (void)hipSetDevice(S->device);
     if (S->stream) (void)hipStreamSynchronize(S->stream);
     // the neighbours' blocks stay mapped (comm_import) and this slab's block goes back to the pool
-    if (S->comm) comm_return(S->comm);
+    if (S->comm) {
+        comm_return(S->comm);
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        --g_live_slabs;
+    }
     S->comm = nullptr;
     (void)hipFree(S->cell_mem);
     (void)hipFree(S->alt_mem);
@@ -2051,6 +2090,9 @@ int sdfgen_hip_release(void)
         delete w;
     }
     g_ws.clear();
+    // imported neighbour blocks (Z-slabs over IPC): closed once no slab session is alive; the pool of
+    // uncached communication blocks is kept (freeing them is what the pool avoids)
+    comm_close_imports();
     return 0;
 }
 

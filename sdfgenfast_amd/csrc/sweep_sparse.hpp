@@ -109,6 +109,14 @@ static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least
                            // Measured neutral (round 5: C3 second pass 2.951-2.962 vs 2.957-2.969 ms,
                            // C4 12.22-12.28 vs 12.21-12.22 ms, profiles/r05b_ab_directpoll.log): off
 #endif
+#ifndef SP_BUSY_NO_TAIL
+#define SP_BUSY_NO_TAIL 0   // with SP_DIRECT_POLL: a wave with an evaluating lane skips the tail read (it only
+                            // decides the drain, and a busy wave cannot leave this iteration anyway)
+#endif
+static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs the direct slot poll");
+#ifndef SP_SINGLE_PASS
+#define SP_SINGLE_PASS 1   // sp_eval_w: a pass in which no lane has a second candidate evaluates one distance per lane
+#endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
@@ -305,13 +313,21 @@ __device__ __forceinline__ unsigned long long sp_eval_w(const SpParams &P, int i
             ta = (qa == q) ? lab[q] : ta;
             tb = (qb == q) ? lab[q] : tb;
         }
-        const size_t ba = 3 * SDF_CHK(26, (has_a ? ta : 0), 0, P.ntri),
-                     bb = 3 * SDF_CHK(26, (has_b ? tb : (has_a ? ta : 0)), 0, P.ntri);
+        const size_t ba = 3 * SDF_CHK(26, (has_a ? ta : 0), 0, P.ntri);
         const float4 a0 = P.soup[ba], a1 = P.soup[ba + 1], a2 = P.soup[ba + 2];
-        const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
-        float da, db;
-        ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w, gx,
-                  mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), b2.w, da, db);
+        float da, db = 0.f;
+#if SP_SINGLE_PASS
+        if (!__any(has_b)) {
+            // no lane has a second candidate left: one distance per lane (ptd_wave, ~2/3 of a packed pass)
+            da = ptd_wave(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w);
+        } else
+#endif
+        {
+            const size_t bb = 3 * SDF_CHK(26, (has_b ? tb : (has_a ? ta : 0)), 0, P.ntri);
+            const float4 b0 = P.soup[bb], b1 = P.soup[bb + 1], b2 = P.soup[bb + 2];
+            ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w, gx,
+                      mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), b2.w, da, db);
+        }
         if (has_a && da < phi) {
             phi = da;
             ct = ta;
@@ -783,9 +799,11 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             vpoll = sp_ld32(ring + sp_slot(h, P.cap));
         // the shard's tail word, read once for the wave's waiting lanes
         unsigned long long qw = 0;
-        if (__any(!done && e == NONE && waiting && !(SLAB && in_role))) {
+        bool tail_read = false;   // wave-uniform
+        if (__any(!done && e == NONE && waiting && !(SLAB && in_role)) && !(SP_BUSY_NO_TAIL && __any(e != NONE))) {
             if (lane == 0) qw = sp_ld64(q_tail);
             qw = ((unsigned long long)(unsigned)__shfl((int)(qw >> 32), 0) << 32) | (unsigned)__shfl((int)qw, 0);
+            tail_read = true;
         }
         SP_IP(1);
 #if SP_SPLIT_APPEND
@@ -837,7 +855,8 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
                 rq = 1;
                 waiting = false;
                 spins = 0;
-            } else if ((qw >> 32) == 0ull && (!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= (unsigned long long)SP_INLANES)) {
+            } else if (tail_read && (qw >> 32) == 0ull &&
+                       (!SLAB || !P.in_ring || sp_ld64(&P.ctl[SP_INDONE]) >= (unsigned long long)SP_INLANES)) {
                 done = true;   // nothing queued or running in this shard (nor to come): no slot can fill any more
             } else if (++spins > SP_WATCHDOG) {
                 atomicOr(&P.ctl[SP_ERR], 1ull);
