@@ -104,18 +104,26 @@ constexpr unsigned SP_INLANES = 64u;   // Z-slab inbound-ring workers (workgroup
 #endif
 static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least one ring lane");
 #ifndef SP_DIRECT_POLL
-#define SP_DIRECT_POLL 0   // k_sp_recheck: a waiting ring lane polls its slot in the same round trip as the
+#define SP_DIRECT_POLL 1   // k_sp_recheck: a waiting ring lane polls its slot in the same round trip as the
                            // wave's tail read (the tail only decides the shard's drain), not after it.
-                           // Measured neutral (round 5: C3 second pass 2.951-2.962 vs 2.957-2.969 ms,
-                           // C4 12.22-12.28 vs 12.21-12.22 ms, profiles/r05b_ab_directpoll.log): off
+                           // Alone neutral (round 5: C3 second pass 2.951-2.962 vs 2.957-2.969 ms,
+                           // profiles/r05b_ab_directpoll.log); what it enables, SP_BUSY_NO_TAIL, is not
 #endif
 #ifndef SP_BUSY_NO_TAIL
-#define SP_BUSY_NO_TAIL 0   // with SP_DIRECT_POLL: a wave with an evaluating lane skips the tail read (it only
-                            // decides the drain, and a busy wave cannot leave this iteration anyway)
+#define SP_BUSY_NO_TAIL 1   // with SP_DIRECT_POLL: a wave with an evaluating lane skips the tail read (it only
+                            // decides the drain, and a busy wave cannot leave this iteration anyway): second
+                            // pass C3 2.82-2.85 -> 2.73-2.76 ms, C4 11.85-12.18 -> 11.45-11.65 ms
+                            // (profiles/r05h_ab_repair_c{3,4}.log, interleaved, with SP_SINGLE_PASS)
+#endif
+#ifndef SP_BUSY_NO_TICKET
+#define SP_BUSY_NO_TICKET 0 // a wave with an evaluating lane takes no new ring tickets (lanes holding one keep
+                            // polling their slot)
 #endif
 static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs the direct slot poll");
 #ifndef SP_SINGLE_PASS
 #define SP_SINGLE_PASS 1   // sp_eval_w: a pass in which no lane has a second candidate evaluates one distance per lane
+                          // (second pass C3 2.95-2.97 -> 2.82-2.85 ms, C4 11.99-12.33 -> 11.85-12.18 ms,
+                          // profiles/r05h_ab_repair_c{3,4}.log)
 #endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
@@ -779,7 +787,8 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
 #endif
         {
             // queue tickets for every lane that needs one: ONE atomic on the head word per wave
-            const bool want = !done && e == NONE && !waiting && !(SLAB && in_role) && !local;
+            const bool busy_wave = SP_BUSY_NO_TICKET && __any(e != NONE);   // (wave-uniform, all lanes)
+            const bool want = !done && e == NONE && !waiting && !(SLAB && in_role) && !local && !busy_wave;
             const unsigned long long wm = __ballot(want);
             if (wm) {
                 unsigned long long base = 0;
