@@ -114,8 +114,9 @@ def _load():
     L.sdfgen_hip_abi_version.restype = ctypes.c_int
     L.sdfgen_hip_build_id.restype = ctypes.c_char_p
     L.sdfgen_hip_device_count.restype = ctypes.c_int
-    L.sdfgen_hip_topology.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), _P, _P]
-    L.sdfgen_hip_topology.restype = ctypes.c_int
+    if hasattr(L, "sdfgen_hip_topology"):   # (absent from pre-ABI-4 libraries loaded for A/B comparisons)
+        L.sdfgen_hip_topology.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_int), _P, _P]
+        L.sdfgen_hip_topology.restype = ctypes.c_int
     L.sdfgen_hip_make_level_set3.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
                                              ctypes.c_char_p, ctypes.c_size_t]
