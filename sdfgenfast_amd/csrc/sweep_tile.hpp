@@ -671,16 +671,12 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     // step is issue-latency bound: -3 % first pass at 256^3)
                     __builtin_amdgcn_s_setprio(0);
                     if (++polls > ST_WATCHDOG || lds_ld(&s_abort)) {
-                        if (polls > ST_WATCHDOG) {
-                            // the stuck task and the lowest a still waiting on halo entries, for
-                            // st_watchdog_report: err[3] = task + 1 (the first failure only), err[10] = a + 1
-                            int am = (act && !(min(rA, min(rB, rC)) > a)) ? a : 0x7fffffff;
-#pragma unroll
-                            for (int d_ = 1; d_ < 64; d_ <<= 1) am = min(am, __shfl_xor(am, d_));
-                            if (L == 0) {
-                                if (atomicCAS(P.err + 3, 0, task + 1) == 0) atomicExch(P.err + 10, am == 0x7fffffff ? 0 : am + 1);
-                                st_fail(P, 2);
-                            }
+                        // the stuck task and its step, for st_watchdog_report: err[3] = task + 1 (the first
+                        // failure only), err[10] = h + 1 (lane 0 alone: a per-lane reduction here cost the
+                        // step loop 2 spilled VGPRs and ~2 % of the first pass, round 5)
+                        if (polls > ST_WATCHDOG && L == 0) {
+                            if (atomicCAS(P.err + 3, 0, task + 1) == 0) atomicExch(P.err + 10, h + 1);
+                            st_fail(P, 2);
                         }
                         if (L == 0) lds_st(&s_abort, 1);
                         h = nsteps;
@@ -2180,18 +2176,21 @@ inline void st_watchdog_report(const TileSweepWorkspace &W, const char *who)
         ++shown;
     }
     // the stuck compute wave's halo entries at a = amin: the granules the helper polls
-    // (k_sweep_tile's compute-wave watchdog records them: err[3] = ctrl[4] = task + 1, err[10] = ctrl[11] = a + 1)
-    const int task = ctrl[4] - 1, amin = ctrl[11] - 1;
-    if ((ctrl[3] >> 8) == 2 && task >= 0 && task < n && amin >= 0 && amin < W.last_A) {
+    // (k_sweep_tile's compute-wave watchdog records them: err[3] = ctrl[4] = task + 1, err[10] = ctrl[11] = step + 1;
+    // the halo entry a cell (bl, cl) reads at step h is a = h - bl - cl: stream L of the b-edge (bl = 0, cl = L)
+    // a = h - L, of the c-edge (cl = 0, bl = L - 8) a = h - (L - 8), the corner a = h)
+    const int task = ctrl[4] - 1, hstep = ctrl[11] - 1;
+    if ((ctrl[3] >> 8) == 2 && task >= 0 && task < n && hstep >= 0) {
         const int J = tk[task].x, K = tk[task].y, q = tk[task].z;
         const unsigned eq = W.epoch - (unsigned)(W.last_ns - 1 - q);   // slot q's epoch (one per sweep, in order)
         const int A = W.last_A, B = W.last_B, hbC = W.last_hbC[q], nK = W.last_nK[q];
-        fprintf(stderr, "  task %d = tile (J %d, K %d) of slot %d (epoch %u), nJ %d nK %d, halo granules at a = %d:\n", task,
-                J, K, q, eq, W.last_nJ, nK, amin);
-        auto show = [&](const char *what, const unsigned long long *base, size_t idx) {
+        fprintf(stderr, "  task %d = tile (J %d, K %d) of slot %d (epoch %u), nJ %d nK %d, stuck at step %d; halo granules:\n",
+                task, J, K, q, eq, W.last_nJ, nK, hstep);
+        auto show = [&](const char *what, const unsigned long long *base, size_t row, int a) {
+            if (a < 0 || a >= A) return;   // that stream is not read at this step
             unsigned long long g = 0;
-            if (hipMemcpy(&g, base + idx, 8, hipMemcpyDeviceToHost) != hipSuccess) return;
-            fprintf(stderr, "    %-30s epoch %u label %d%s\n", what, (unsigned)(g >> 32), lbl_of((uint32_t)g),
+            if (hipMemcpy(&g, base + row * A + a, 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+            fprintf(stderr, "    %-30s a = %5d: epoch %u label %d%s\n", what, a, (unsigned)(g >> 32), lbl_of((uint32_t)g),
                     (unsigned)(g >> 32) == eq ? " (ready)" : " (NOT ready)");
         };
         const unsigned long long *hb = W.mhb + (size_t)q * W.last_nhb, *hc = W.mhc + (size_t)q * W.last_nhc;
@@ -2200,14 +2199,14 @@ inline void st_watchdog_report(const TileSweepWorkspace &W, const char *who)
         if (J > 0)
             for (int L = 0; L < ST_T && c0 + L < hbC; ++L) {
                 snprintf(buf, sizeof(buf), "b-edge stream %d (c %d)", L, c0 + L);
-                show(buf, hb, ((size_t)(J - 1) * hbC + (c0 + L)) * A + amin);
+                show(buf, hb, (size_t)(J - 1) * hbC + (c0 + L), hstep - L);
             }
         if (K > 0)
             for (int L = 0; L < ST_T && b0 + L < B; ++L) {
                 snprintf(buf, sizeof(buf), "c-edge stream %d (b %d)", ST_T + L, b0 + L);
-                show(buf, hc, ((size_t)(K - 1) * B + (b0 + L)) * A + amin);
+                show(buf, hc, (size_t)(K - 1) * B + (b0 + L), hstep - L);
             }
-        if (J > 0 && K > 0) show("corner stream 16", hb, ((size_t)(J - 1) * hbC + (c0 - 1)) * A + amin);
+        if (J > 0 && K > 0) show("corner stream 16", hb, (size_t)(J - 1) * hbC + (c0 - 1), hstep);
     }
 }
 
