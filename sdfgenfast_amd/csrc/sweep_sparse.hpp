@@ -120,6 +120,10 @@ static_assert(SP_LOCAL_LANES >= 0 && SP_LOCAL_LANES < 64, "a wave keeps at least
                             // polling their slot)
 #endif
 static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs the direct slot poll");
+#ifndef SP_LATE_APPEND
+#define SP_LATE_APPEND 0   // k_sp_recheck (SP_SPLIT_APPEND): wait for the previous iteration's append atomic at the
+                           // end of this iteration instead of before the evaluation (its ring slots fill later)
+#endif
 #ifndef SP_SINGLE_PASS
 #define SP_SINGLE_PASS 1   // sp_eval_w: a pass in which no lane has a second candidate evaluates one distance per lane
                           // (second pass C3 2.95-2.97 -> 2.82-2.85 ms, C4 11.99-12.33 -> 11.85-12.18 ms,
@@ -815,7 +819,7 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
             tail_read = true;
         }
         SP_IP(1);
-#if SP_SPLIT_APPEND
+#if SP_SPLIT_APPEND && !SP_LATE_APPEND
         sp_append_finish(P, shard, tgt_app, app);   // last iteration's append (its atomic overlapped the above)
 #endif
         SP_IP(2);
@@ -957,6 +961,9 @@ __global__ void __launch_bounds__(64) k_sp_recheck(SpParams P)
         const bool idle_local = local && e == NONE && !(SLAB && in_role);
         SP_IP(7);
 #if SP_SPLIT_APPEND
+#if SP_LATE_APPEND
+        sp_append_finish(P, shard, tgt_app, app);   // last iteration's append: its atomic overlapped this whole iteration
+#endif
         sp_append_issue(P, shard, qmask, fin, nloc, app);
         SP_IP(8);
         if (app.live) {
