@@ -156,6 +156,15 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 #ifndef BAND_LDS_DEF
 #define BAND_LDS_DEF 5120
 #endif
+#ifndef BAND_FDIV
+#define BAND_FDIV 1      // box coordinates by float reciprocal + one exact correction: band 0.797 -> 0.765 ms at C3
+#endif
+#ifndef BAND_WQ
+#define BAND_WQ 1        // triangle of a pair by a wave-wide search (no binary search): with FDIV 0.797 -> 0.676 ms at C3, 1.30 -> 1.19 at C4
+#endif
+// diagnostics only (wrong results): BAND_DIAG_NOPTD (a pair's distance without the point-triangle
+// evaluation), BAND_DIAG_NOFLUSH (no global atomics from the LDS table), BAND_DIAG_NOPAIR (no pairs:
+// the batches' set-up, ray parity, table initialisation and barriers)
 constexpr int BAND_BT = BAND_BT_DEF;    // triangles per batch (<= 64: one wave sets a batch up)
 constexpr int BAND_LDS = BAND_LDS_DEF;  // u64 keys in the LDS table (40 KB)
 static_assert(BAND_BT >= 1 && BAND_BT <= 64, "a batch's boxes are scanned by one wave");
@@ -247,6 +256,22 @@ __device__ __forceinline__ int find_q(const unsigned *pre, int nb, unsigned fl)
 #pragma unroll
     for (int step = BAND_BT / 2; step >= 1; step >>= 1)
         if (q + step < nb && pre[q + step] <= fl) q += step;
+    return q;
+}
+
+// The same q for a wave whose lanes carry consecutive flat indices F + lane: lane x holds pre[x]
+// (lanes >= nb: UINT_MAX).  The offsets at or below F give lane 0's triangle; each offset inside
+// (F, F + 63] -- usually none or one, a box holding ~90 cells -- moves the lanes at or past it on.
+__device__ __forceinline__ int band_wq(unsigned pl, unsigned F, unsigned lane)
+{
+    int q = __popcll(__ballot(pl <= F)) - 1;
+    unsigned long long m = __ballot(pl > F && pl - F <= 63u);
+    const unsigned fl = F + lane;
+    while (m) {
+        const int b = __ffsll((long long)m) - 1;
+        q += fl >= (unsigned)__builtin_amdgcn_readlane((int)pl, b) ? 1 : 0;
+        m &= m - 1;
+    }
     return q;
 }
 
@@ -348,16 +373,30 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
             parity_point(s_f[q], L.j0 + (int)(r - kk * (unsigned)L.nj), L.k0 + (int)kk, g, cnt);
         }
         __syncthreads();
-        // (triangle, cell) pair of flat index fl
-        auto pair_of = [&](unsigned fl, int &i, int &j, int &k, uint64_t &t) {
-            const int q = find_q(s_pre, nb, fl);
+        // (triangle, cell) pair of flat index fl (triangle q of the batch)
+        auto pair_in = [&](int q, unsigned fl, int &i, int &j, int &k) {
             const BandBox B = s_box[q];
             const unsigned r = fl - s_pre[q], bij = (unsigned)(B.bi * B.bj);
+#if BAND_FDIV
+            // r < bi*bj*bk <= BAND_BIG_VOL (a small triangle's box): the float quotient is within 1 of
+            // the exact one (|error| < 4096 * 2^-22), and one signed correction makes it exact
+            auto qdiv = [](unsigned x, unsigned d, unsigned &rm) {
+                int qq = (int)((float)x * __builtin_amdgcn_rcpf((float)d));
+                int rr = (int)x - qq * (int)d;
+                qq = rr < 0 ? qq - 1 : (rr >= (int)d ? qq + 1 : qq);
+                rr = rr < 0 ? rr + (int)d : (rr >= (int)d ? rr - (int)d : rr);
+                rm = (unsigned)rr;
+                return (unsigned)qq;
+            };
+            unsigned rem, ii;
+            const unsigned kk = qdiv(r, bij, rem), jj = qdiv(rem, (unsigned)B.bi, ii);
+            i = B.i0 + (int)ii;
+#else
             const unsigned kk = r / bij, rem = r - kk * bij, jj = rem / (unsigned)B.bi;
             i = B.i0 + (int)(rem - jj * (unsigned)B.bi);
+#endif
             j = B.j0 + (int)jj;
             k = B.k0 + (int)kk;
-            t = t0 + q;
         };
         auto emit = [&](float d, int i, int j, int k, uint64_t t) {
             if (d < init) {   // also rejects NaN
@@ -370,26 +409,53 @@ __global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ sou
                 }
             }
         };
-        // two pairs per lane (fl, fl + 256) evaluated together in packed FP32 (ptd_wave2)
-        for (unsigned fl = tid; fl < total; fl += 512) {
-            const bool two = fl + 256 < total;
-            int i, j, k, i2, j2, k2;
-            uint64_t t, t2;
-            pair_of(fl, i, j, k, t);
-            pair_of(two ? fl + 256 : fl, i2, j2, k2, t2);
-            const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
-            const f3 gx2 = mk3((float)i2 * g.dx + g.ox, (float)j2 * g.dx + g.oy, (float)k2 * g.dx + g.oz);
-            float d, d2 = 0.0f;
-            if (__any(two)) {
-                ptd_wave2(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2), soup[3 * t + 2].w, gx2,
-                          load_vtx(soup, t2, 0), load_vtx(soup, t2, 1), load_vtx(soup, t2, 2), soup[3 * t2 + 2].w, d, d2);
-            } else {
-                d = ptd_wave(gx, load_vtx(soup, t, 0), load_vtx(soup, t, 1), load_vtx(soup, t, 2), soup[3 * t + 2].w);
+        // two pairs per lane (F + L and F + 256 + L for lane L of a wave at F, a wave-uniform loop),
+        // evaluated together in packed FP32 (ptd_wave2)
+        {
+            const unsigned lane = (unsigned)tid & 63u;
+#if BAND_WQ
+            const unsigned pl = lane < (unsigned)nb ? s_pre[lane] : 0xffffffffu;
+#endif
+#if BAND_DIAG_NOPAIR
+            if (false)
+#endif
+            for (unsigned F = (unsigned)tid - lane; F < total; F += 512) {
+                const unsigned fa = F + lane, fb = fa + 256;
+                const bool one = fa < total, two = fb < total;
+#if BAND_WQ
+                // both searches by the whole wave (their ballots need every lane), then selected
+                const int qa = band_wq(pl, F, lane), qb0 = band_wq(pl, F + 256, lane);
+                const int qb = two ? qb0 : qa;
+#else
+                const int qa = find_q(s_pre, nb, fa), qb = two ? find_q(s_pre, nb, fb) : qa;
+#endif
+                int i, j, k, i2, j2, k2;
+                pair_in(qa, fa, i, j, k);
+                pair_in(qb, two ? fb : fa, i2, j2, k2);
+                const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
+                const f3 gx2 = mk3((float)i2 * g.dx + g.ox, (float)j2 * g.dx + g.oy, (float)k2 * g.dx + g.oz);
+                const float4 *sa = soup + 3 * (t0 + qa), *sb = soup + 3 * (t0 + qb);
+                const float4 a0 = sa[0], a1 = sa[1], a2 = sa[2], b0 = sb[0], b1 = sb[1], b2 = sb[2];
+                float d, d2 = 0.0f;
+#if BAND_DIAG_NOPTD
+                d = (float)(i + j + k) * g.dx + a0.x * 0.0f;
+                d2 = (float)(i2 + j2 + k2) * g.dx + b0.x * 0.0f;
+#else
+                if (__any(two)) {
+                    ptd_wave2(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w, gx2,
+                              mk3(b0.x, b0.y, b0.z), mk3(b1.x, b1.y, b1.z), mk3(b2.x, b2.y, b2.z), b2.w, d, d2);
+                } else {
+                    d = ptd_wave(gx, mk3(a0.x, a0.y, a0.z), mk3(a1.x, a1.y, a1.z), mk3(a2.x, a2.y, a2.z), a2.w);
+                }
+#endif
+                if (one) emit(d, i, j, k, t0 + qa);
+                if (two) emit(d2, i2, j2, k2, t0 + qb);
             }
-            emit(d, i, j, k, t);
-            if (two) emit(d2, i2, j2, k2, t2);
         }
         __syncthreads();
+#if BAND_DIAG_NOFLUSH
+        if (false)
+#endif
         if (merge)
             for (unsigned c = tid; c < uvol; c += 256) {
                 const u64 key = s_key[c];
@@ -972,8 +1038,10 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     if (impl == 1 && ws->wf.trace_sweep < 0) {
         const char *e = getenv("SDFGEN_TILE_MULTI");
         const int want = std::min(std::min(sparse_first, nsweeps), 8);
-        const double bytes = 8.0 * want * (((nj - 1 + 7) / 8) * (double)(nk - 1) + ((nk - 1 + 7) / 8) * (double)(nj - 1)) *
-                             (double)(ni - 1);
+        // (wide halo entries: st_halo_gran granules of 8 bytes per entry)
+        const long long tiles = (long long)((nj - 1 + 7) / 8) * ((nk - 1 + 7) / 8);
+        const double bytes = 8.0 * st_halo_gran(st_cfg(tiles), 1) * want *
+                             (((nj - 1 + 7) / 8) * (double)(nk - 1) + ((nk - 1 + 7) / 8) * (double)(nj - 1)) * (double)(ni - 1);
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const double have = (double)free_b + (double)ws->wf.cap_mhb * 8.0 + (double)ws->wf.cap_mhc * 8.0;
