@@ -1038,10 +1038,8 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     if (impl == 1 && ws->wf.trace_sweep < 0) {
         const char *e = getenv("SDFGEN_TILE_MULTI");
         const int want = std::min(std::min(sparse_first, nsweeps), 8);
-        // (wide halo entries: st_halo_gran granules of 8 bytes per entry)
-        const long long tiles = (long long)((nj - 1 + 7) / 8) * ((nk - 1 + 7) / 8);
-        const double bytes = 8.0 * st_halo_gran(st_cfg(tiles), 1) * want *
-                             (((nj - 1 + 7) / 8) * (double)(nk - 1) + ((nk - 1 + 7) / 8) * (double)(nj - 1)) * (double)(ni - 1);
+        const double bytes = 8.0 * want * (((nj - 1 + 7) / 8) * (double)(nk - 1) + ((nk - 1 + 7) / 8) * (double)(nj - 1)) *
+                             (double)(ni - 1);
         size_t free_b = 0, total_b = 0;
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
         const double have = (double)free_b + (double)ws->wf.cap_mhb * 8.0 + (double)ws->wf.cap_mhc * 8.0;

@@ -189,30 +189,6 @@ inline int st_cfg(long long tiles)
     if (const char *e = getenv("SDFGEN_TILE_CFG")) return std::max(0, std::min(5, atoi(e)));
     return tiles > ST_QUAD_MAX_TILES ? ST_CFG_THR : ST_CFG_QUAD;
 }
-
-// Wide halo entries (quad tiles in the one-GPU multi-sweep launch): a tile-edge cell's result travels
-// to the downstream tile as ST_WG tagged 8-byte granules -- its low word, then the winner triangle's
-// x1.xyz, x2.xyz, x3.xyzw (one spare) -- so the consumer's helper lands a halo entry as soon as its
-// poll returns, without the vertex gather that a label-only granule needs (one global round trip less
-// per tile hop; DESIGN.md §4 "wide halo entries").  Every granule carries the sweep's epoch, so a
-// consumer that sees all eleven tags has the whole entry, whatever order the stores landed in.
-#ifndef ST_WIDE
-#define ST_WIDE 0
-#endif
-constexpr int ST_WG = 12;    // granules per wide halo entry: entry word m in granule m (96 B)
-constexpr int ST_WUSE = 11;  // granules a consumer needs (all but granule 7: the phi word, unused in a halo)
-constexpr int ST_WLBL = 3;   // the granule of the low word (label)
-typedef unsigned int st_u4 __attribute__((ext_vector_type(4)));
-// a raw buffer resource over [p, p + 2 GB) built from wave-uniform halves (no waterfall loops)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t st_rsrc(const void *p)
-{
-    const unsigned long long u = (unsigned long long)(uintptr_t)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
-    return __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)(((unsigned long long)hi << 32) | lo), (short)0, 0x7fffffff,
-                                             0x00020000);
-}
-// granules per halo entry of a multi-sweep launch with this configuration and slab count
-inline int st_halo_gran(int cfg, int nslabs) { return (ST_WIDE && nslabs == 1 && cfg == ST_CFG_QUAD) ? ST_WG : 1; }
 inline bool st_use_thr(long long tiles) { return st_cfg(tiles) == ST_CFG_THR; }
 
 constexpr unsigned ST_WATCHDOG = 1u << 24;    // empty polls before giving up (~seconds)
@@ -401,9 +377,6 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     constexpr bool TWIN = Cfg::TWIN;
     StParams P = P0;
     constexpr int GSCOPE = SLAB ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT;
-    // wide halo entries (st_halo_gran): the quad tiles of a one-GPU multi-sweep launch
-    constexpr bool WIDE = ST_WIDE && MULTI && !SLAB && Cfg::LPC == 4 && !Cfg::FIX;
-    constexpr int HSTR = WIDE ? ST_WG : 1;   // granules per halo entry
     __shared__ float4 s_ent[ST_ENTS * 3];   // entry e: [3e] = (x1, label), [3e+1] = (x2, phi), [3e+2] = x3
     // per compute wave (not used by the lanes-per-cell step: one word then):
     // s_pd[w]: [0, 7 CPW) the (entry << 9 | q << 6 | lane) list, [7 CPW, 14 CPW) the distance bits of
@@ -1306,38 +1279,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     if (win >= 0 && ST_DIAG_SPLIT != 1)
                         P.cell[SDF_CHK(5, st_phys(P, a, b, c), P.clo, P.chi)] =
                             ((unsigned long long)__float_as_uint(phi) << 32) | w_new;
-                    if constexpr (WIDE) {
-                        // the whole entry, in entry order, as 12 tagged granules -- two per 16-byte write-through
-                        // store (cdna_hip_programming.md G16 pitfall 7: narrow sc1 stores of bulk data are slow)
-                        const uint32_t ep = P.epoch;
-                        const st_u4 d0 = {__float_as_uint(w0.x), ep, __float_as_uint(w0.y), ep};
-                        const st_u4 d1 = {__float_as_uint(w0.z), ep, w_new, ep};
-                        const st_u4 d2 = {__float_as_uint(w1.x), ep, __float_as_uint(w1.y), ep};
-                        const st_u4 d3 = {__float_as_uint(w1.z), ep, __float_as_uint(w1.w), ep};
-                        const st_u4 d4 = {__float_as_uint(w2.x), ep, __float_as_uint(w2.y), ep};
-                        const st_u4 d5 = {__float_as_uint(w2.z), ep, __float_as_uint(w2.w), ep};
-                        auto put = [&](unsigned long long *buf, size_t ent) {
-                            const __amdgpu_buffer_rsrc_t r = st_rsrc(buf);
-                            const int o = (int)(ent * (ST_WG * 8));
-                            __builtin_amdgcn_raw_buffer_store_b128(d0, r, o, 0, 16);   // aux 16: sc1
-                            __builtin_amdgcn_raw_buffer_store_b128(d1, r, o + 16, 0, 16);
-                            __builtin_amdgcn_raw_buffer_store_b128(d2, r, o + 32, 0, 16);
-                            __builtin_amdgcn_raw_buffer_store_b128(d3, r, o + 48, 0, 16);
-                            __builtin_amdgcn_raw_buffer_store_b128(d4, r, o + 64, 0, 16);
-                            __builtin_amdgcn_raw_buffer_store_b128(d5, r, o + 80, 0, 16);
-                        };
-                        if (bl == ST_T - 1 && J < P.nJ - 1) put(P.hb, ((size_t)J * P.hbC + (c - P.cs)) * P.A + a);
-                        if (cl == ST_T - 1 && K < P.nK - 1) put(P.hc, ((size_t)K * P.B + b) * P.A + a);
-                    } else {
-                        const unsigned long long gran = st_granule(P.epoch, w_new);
-                        if (bl == ST_T - 1 && J < P.nJ - 1)
-                            __hip_atomic_store(P.hb + ((size_t)J * P.hbC + (c - P.cs)) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
-                        if (cl == ST_T - 1 && K < P.nK - 1)
-                            __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
-                        if (SLAB && P.hc_out && c == P.ce - 1)
-                            __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_SYSTEM);
-                    }
+                    const unsigned long long gran = st_granule(P.epoch, w_new);
+                    if (bl == ST_T - 1 && J < P.nJ - 1)
+                        __hip_atomic_store(P.hb + ((size_t)J * P.hbC + (c - P.cs)) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                    if (cl == ST_T - 1 && K < P.nK - 1)
+                        __hip_atomic_store(P.hc + ((size_t)K * P.B + b) * P.A + a, gran, __ATOMIC_RELAXED, GSCOPE);
+                    if (SLAB && P.hc_out && c == P.ce - 1)
+                        __hip_atomic_store(P.hc_out + st_inbox(P, a, b), gran, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
                 }
                 }   // LPC != 8
                 if (TRACE && P.trace) {
@@ -1390,17 +1339,17 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             if (hlane) {
                 if (L < ST_T) {
                     hbs = b0 - 1; hcs = c0 + L; hoff = L; hvalid = hcs < P.ce; hbound = (J == 0);
-                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.hbC + (hcs - P.cs)) * P.A * HSTR;
+                    if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.hbC + (hcs - P.cs)) * P.A;
                 } else if (L < 2 * ST_T) {
                     hbs = b0 + (L - ST_T); hcs = c0 - 1; hoff = L - ST_T; hvalid = hbs < P.B;
                     hbound = (K == 0) && !inbox;
                     if (inbox) hsrc = P.hc_in + st_inbox(P, 0, hbs);
-                    else if (!hbound) hsrc = P.hc + ((size_t)(K - 1) * P.B + hbs) * P.A * HSTR;
+                    else if (!hbound) hsrc = P.hc + ((size_t)(K - 1) * P.B + hbs) * P.A;
                 } else {
                     hbs = b0 - 1; hcs = c0 - 1; hoff = 0; hvalid = true;
                     hbound = (J == 0 || K == 0) && !inbox;
                     if (inbox) hsrc = P.hc_in + st_inbox(P, 0, hbs);
-                    else if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.hbC + (hcs - P.cs)) * P.A * HSTR;
+                    else if (!hbound) hsrc = P.hb + ((size_t)(J - 1) * P.hbC + (hcs - P.cs)) * P.A;
                 }
             }
             if (!hvalid || hbound) hsrc = P.hb;   // any valid address: unused lanes load harmlessly
@@ -1435,284 +1384,29 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             unsigned long long hp_n = 0, hp_cyc = 0, hp_own = 0, hp_halo = 0, hp_t0 = 0;
 #endif
             bool tr_halo = false, tr_own = false;   // TRACE + MULTI: first landings recorded
-            // The helper loop, in two forms when wide halo entries are on: a task of an inner tile (J, K > 0)
-            // has no boundary stream, so all its halo lanes land wide entries and its loop issues no halo
-            // gathers (their 24 registers spilled); an edge tile polls the label granules and gathers.
-            auto hloop = [&](auto hw_tag) {
-                constexpr bool HW = decltype(hw_tag)::value;
-                // WIDE: a halo lane whose stream comes from a tile of this sweep (not a boundary plane) lands
-                // its entries straight from the wide granules.  The 187 granules of one halo slot (17 streams
-                // x 11) are spread over three loads of the whole wave -- load k of lane L takes granule
-                // x = 64 k + L: stream x / 11, part x % 11 -- so each load instruction touches a few
-                // consecutive lines instead of one line per stream.
-                const bool hwide = HW && hlane && hvalid;   // (no boundary stream in a wide task)
-                // per load k: wd_k = stream | entry word (0..11) << 8 | 1 << 12 if the stream is wide, and wg_k = the
-                // granule's element offset from P.hb (b-edge and corner streams) or P.hc (c-edge, bit 31)
-                int wd0 = ST_NSTREAM - 1, wd1 = ST_NSTREAM - 1, wd2 = ST_NSTREAM - 1;
-                uint32_t wg0 = 0, wg1 = 0, wg2 = 0;
-                if constexpr (HW) {
-                    const int hw = hwide ? 1 : 0;
-                    // the stream's first granule as an offset (hb and hc hold < 2^31 granules: st_halo_gran)
-                    const uint32_t off = (uint32_t)(hsrc - (L >= ST_T && L < 2 * ST_T ? P.hc : P.hb)) | (L >= ST_T && L < 2 * ST_T ? 0x80000000u : 0u);
-                    // part p of a stream's entry: granule (= entry word) p < 7 ? p : p + 1 -- word 7, the phi
-                    // word, is never read from a halo entry
-                    auto part = [&](int x, int &wd, uint32_t &wg) {
-                        const bool in = x < ST_NSTREAM * ST_WUSE;
-                        const int ws = in ? x / ST_WUSE : ST_NSTREAM - 1;
-                        const int wp = x - ws * ST_WUSE;                // part 0..10
-                        const int wm = wp < 7 ? wp : wp + 1;            // granule = entry word (7, phi: not sent)
-                        const int wo = in ? wm : 0;                     // <= 11
-                        const bool wk = in && __shfl(hw, ws) != 0;
-                        wd = ws | (wo << 8) | (wk ? 1 << 12 : 0);   // (x >= 187 once put word 16 into the flag bit)
-                        wg = (uint32_t)__shfl((int)off, ws) + (uint32_t)wm;
-                    };
-                    part(L, wd0, wg0);
-                    part(64 + L, wd1, wg1);
-                    part(128 + L, wd2, wg2);
-                }
-                // batch A of the spread loads: slot g, load k (named registers, as c0..q3 below)
-                unsigned long long v00 = 0, v01 = 0, v02 = 0, v10 = 0, v11 = 0, v12 = 0;
-                int wa0 = 0, wa1 = 0, wa2 = 0;   // the stream's batch A: first entry << 3 | count
-                for (;;) {
-                    // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
-                    // may finish step h while wave w-1 is still on step h (it needs only h-1 of it).
-                    int prog = lds_ld(&s_hdr[1]);
+            for (;;) {
+                // Ring capacity follows the slowest compute wave.  Not simply the last one: wave w
+                // may finish step h while wave w-1 is still on step h (it needs only h-1 of it).
+                int prog = lds_ld(&s_hdr[1]);
 #pragma unroll
-                    for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_hdr[1 + w]));
-                    if (lds_ld(&s_abort)) break;
-                    // (wide tasks: only when no lane has anything in flight -- the spread loads' ballots and
-                    // shuffles below need the whole wave, and a lane that backs off here would leave it)
-                    if (idle && (HW ? __all(gA == 0 && hcA == 0) : (gA == 0 && hcA == 0))) {
-                        // Nothing in flight and the last round found nothing to do: wait cheaply (LDS
-                        // progress, at most one granule probe per halo lane) instead of running the
-                        // whole pipeline body on dummy loads -- idle helpers steal VALU issue slots
-                        // from the compute waves sharing their SIMD.
-                        if (__all(fA >= nsteps && hA >= P.A)) break;
-                        const int own_n = min(ST_G, min(nsteps - fA, prog + ST_RO - fA));
-                        const int halo_n = hvalid ? min(ST_G, min(P.A - hA, prog + ST_RH - hoff - 2 - hA)) : 0;
-                        bool go = own_n > 0;
-                        if (halo_n > 0)
-                            go = go || hbound ||
-                                 st_granule_ready(__hip_atomic_load(hsrc + (size_t)hA * HSTR + (WIDE ? ST_WLBL : 0), __ATOMIC_RELAXED, GSCOPE), P.epoch);
-                        if (!__any(go)) {
-                            ++n_hpoll;
-                            if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
-                                if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 16); }   // 16: a helper gave up
-                                break;
-                            }
-                            const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
-                            if (idle < 4) __builtin_amdgcn_s_sleep(1);
-                            else if (idle < 16) __builtin_amdgcn_s_sleep(4);
-                            else __builtin_amdgcn_s_sleep(ST_HSLEEP);
-                            if (SLAB && P.tm) t_idle += wall_clock64() - ts;
-                            continue;
-                        }
-                    }
-                    // The batch-A loads were issued one iteration ago: wait for them once, and hand
-                    // the registers back through the asm so the compiler does not track them as
-                    // pending (its per-use waits would otherwise serialise the gathers below).
-                    asm volatile("s_waitcnt vmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(q0), "+v"(q1),
-                                 "+v"(q2), "+v"(q3)::"memory");
-                    if constexpr (HW)
-                        asm volatile("" : "+v"(v00), "+v"(v01), "+v"(v02), "+v"(v10), "+v"(v11), "+v"(v12)::"memory");
-                    // ---- stage 2: vertices for batch A ----
-                    int hp = 0;   // ready prefix of the halo batch (tag == epoch; boundary planes always)
-                    const bool r0 = HW || hbound || st_granule_ready(q0, P.epoch);
-                    const bool r1 = HW || hbound || st_granule_ready(q1, P.epoch);
-                    const bool r2 = HW || hbound || st_granule_ready(q2, P.epoch);
-                    const bool r3 = HW || hbound || st_granule_ready(q3, P.epoch);
-                    bool rw0 = true, rw1 = true;   // WIDE: all 11 granules of the stream's slot-0 / slot-1 entry tagged
-                    if constexpr (HW) {
-                        static_assert(ST_G == 2, "wide halo entries: written for 2-element batches");
-                        // a granule that was requested and does not carry this sweep's epoch holds its entry back
-                        // (wa_k & 7: the stream's requested count, 0 unless the stream is wide)
-                        const unsigned long long b00 = __ballot(!(0 < (wa0 & 7)) || st_granule_ready(v00, P.epoch));
-                        const unsigned long long b01 = __ballot(!(0 < (wa1 & 7)) || st_granule_ready(v01, P.epoch));
-                        const unsigned long long b02 = __ballot(!(0 < (wa2 & 7)) || st_granule_ready(v02, P.epoch));
-                        const unsigned long long b10 = __ballot(!(1 < (wa0 & 7)) || st_granule_ready(v10, P.epoch));
-                        const unsigned long long b11 = __ballot(!(1 < (wa1 & 7)) || st_granule_ready(v11, P.epoch));
-                        const unsigned long long b12 = __ballot(!(1 < (wa2 & 7)) || st_granule_ready(v12, P.epoch));
-                        // bits 11 L .. 11 L + 10 of the 192-bit ballot: stream L's 11 granules
-                        const int x0 = ST_WUSE * (hlane ? L : 0), wd = x0 >> 6, bt = x0 & 63;
-                        auto win = [&](unsigned long long m0, unsigned long long m1, unsigned long long m2) {
-                            const unsigned long long lo = wd == 0 ? m0 : (wd == 1 ? m1 : m2);
-                            const unsigned long long hi = wd == 0 ? m1 : (wd == 1 ? m2 : ~0ull);
-                            const unsigned long long v = (lo >> bt) | (bt ? (hi << (64 - bt)) : 0ull);
-                            return (v & 0x7ffull) == 0x7ffull;
-                        };
-                        rw0 = !hwide || win(b00, b01, b02);
-                        rw1 = !hwide || win(b10, b11, b12);
-                    }
-                    if (0 < hcA && r0 && rw0) { hp = 1; if (1 < hcA && r1 && rw1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
-                    if constexpr (HW) {
-                        // land the wide entries now (no gather to wait for), then publish them
-                        const int hp0 = __shfl(hp, wd0 & 31), hp1 = __shfl(hp, wd1 & 31), hp2 = __shfl(hp, wd2 & 31);
-                        uint32_t *sw = reinterpret_cast<uint32_t *>(s_ent);
-                        auto put = [&](int wd, int hpk, int wa, int g, unsigned long long v) {
-                            if ((wd & (1 << 12)) && g < hpk)
-                                sw[(ST_HALO0 + (wd & 31) * ST_RH + (((wa >> 3) + g) & (ST_RH - 1))) * 12 + ((wd >> 8) & 15)] = (uint32_t)v;
-                        };
-                        put(wd0, hp0, wa0, 0, v00);
-                        put(wd1, hp1, wa1, 0, v01);
-                        put(wd2, hp2, wa2, 0, v02);
-                        put(wd0, hp0, wa0, 1, v10);
-                        put(wd1, hp1, wa1, 1, v11);
-                        put(wd2, hp2, wa2, 1, v12);
-                        lds_drain();
-                        if (hwide && hp) lds_st(&s_halo_ready[L], hA + hp);
-                    }
-#define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
-#define ST_GATHER(g, cg, qg)                                                                          \
-        const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
-        const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
-        const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
-        const float4 z4_##g = make_float4(0.f, 0.f, 0.f, 0.f); /* wide tasks: no halo gathers */                \
-        const float4 ha##g = HW ? z4_##g : P.soup[sh##g], hb##g = HW ? z4_##g : P.soup[sh##g + 1], hc##g = HW ? z4_##g : P.soup[sh##g + 2];
-                    ST_GATHER(0, c0, q0)
-#ifdef ST_OWNDEDUP   // experiment: slot 1 repeating slot 0's label reads the shared dummy line instead
-                    const bool dup1 = ST_OWN_OK(0) && ST_OWN_OK(1) && lbl_of((uint32_t)c1) == lbl_of((uint32_t)c0);
-                    const bool hdup1 = 0 < hp && 1 < hp && lbl_of((uint32_t)q1) == lbl_of((uint32_t)q0);
-                    const size_t so1 = 3 * SDF_CHK(11, (ST_OWN_OK(1) && !dup1 && lbl_of((uint32_t)c1) >= 0 ? lbl_of((uint32_t)c1) : gdum), 0, P.ntri);
-                    const float4 oa1_ = P.soup[so1], ob1_ = P.soup[so1 + 1], oc1_ = P.soup[so1 + 2];
-                    const size_t sh1 = 3 * SDF_CHK(12, (1 < hp && !hdup1 && lbl_of((uint32_t)q1) >= 0 ? lbl_of((uint32_t)q1) : gdum), 0, P.ntri);
-                    const float4 ha1_ = P.soup[sh1], hb1_ = P.soup[sh1 + 1], hc1_ = P.soup[sh1 + 2];
-#else
-                    ST_GATHER(1, c1, q1)
-#endif
-#if ST_G_DEF > 2
-                    ST_GATHER(2, c2, q2)
-                    ST_GATHER(3, c3, q3)
-#endif
-                    // ---- stage 1: issue batch B ----
-                    const int fB = fA + gA;
-                    int gB = min(ST_G, min(nsteps - fB, prog + ST_RO - fB));
-                    if (gB < 0) gB = 0;
-                    const int hB = hA + hp;
-                    int hcB = 0;
-                    if (hvalid) {
-                        hcB = min(ST_G, min(P.A - hB, prog + ST_RH - hoff - 2 - hB));
-                        if (hcB < 0) hcB = 0;
-                    }
-#define ST_ISSUE(g, cn, qn)                                                                            \
-        {                                                                                                  \
-            const int a_ = fB + (g) - bl - cl;                                                             \
-            const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
-            const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
-            cn = P.cell[SDF_CHK(6, ix_, P.clo, P.chi)];                                                    \
-            const unsigned long long *src_ =                                                               \
-                (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
-                           : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + (size_t)(hB + (g)) * HSTR + (WIDE ? ST_WLBL : 0)); \
-            qn = HW ? 0ull : __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE); /* wide: spread loads */    \
-        }
-                    // Always issued (a fixed count keeps the waits below precise); slots with nothing
-                    // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
-                    // not flood the fabric with granule polls.
-                    unsigned long long n0, n1, n2, n3, m0, m1, m2, m3;
-                    ST_ISSUE(0, n0, m0)
-                    ST_ISSUE(1, n1, m1)
-#if ST_G_DEF > 2
-                    ST_ISSUE(2, n2, m2)
-                    ST_ISSUE(3, n3, m3)
-#else
-                    n2 = n3 = ~0ull;
-                    m2 = m3 = 0ull;
-#endif
-                    unsigned long long u00 = 0, u01 = 0, u02 = 0, u10 = 0, u11 = 0, u12 = 0;
-                    int wb0 = 0, wb1 = 0, wb2 = 0;   // the stream's batch B: first entry << 3 | count (0: not wide)
-                    if constexpr (HW) {
-                        const int pk = (hB << 3) | hcB;   // hcB <= 2
-                        wb0 = __shfl(pk, wd0 & 31);
-                        wb1 = __shfl(pk, wd1 & 31);
-                        wb2 = __shfl(pk, wd2 & 31);
-                        wb0 = (wd0 & (1 << 12)) ? wb0 : 0;
-                        wb1 = (wd1 & (1 << 12)) ? wb1 : 0;
-                        wb2 = (wd2 & (1 << 12)) ? wb2 : 0;
-                        const unsigned long long *dm = P.cell + dummy;
-                        auto gp = [&](uint32_t wg, int wb, int g) {
-                            const unsigned long long *base = (wg & 0x80000000u) ? P.hc : P.hb;
-                            return (g < (wb & 7)) ? base + (wg & 0x7fffffffu) + (size_t)((wb >> 3) + g) * ST_WG : dm;
-                        };
-                        u00 = __hip_atomic_load(gp(wg0, wb0, 0), __ATOMIC_RELAXED, GSCOPE);
-                        u01 = __hip_atomic_load(gp(wg1, wb1, 0), __ATOMIC_RELAXED, GSCOPE);
-                        u02 = __hip_atomic_load(gp(wg2, wb2, 0), __ATOMIC_RELAXED, GSCOPE);
-                        u10 = __hip_atomic_load(gp(wg0, wb0, 1), __ATOMIC_RELAXED, GSCOPE);
-                        u11 = __hip_atomic_load(gp(wg1, wb1, 1), __ATOMIC_RELAXED, GSCOPE);
-                        u12 = __hip_atomic_load(gp(wg2, wb2, 1), __ATOMIC_RELAXED, GSCOPE);
-                    }
-#ifdef ST_HALO_DELAY   // diagnostics: the first pass's sensitivity to the tile-hop latency (DESIGN.md §6)
-                    if (__any(hp > 0)) __builtin_amdgcn_s_sleep(ST_HALO_DELAY);
-#endif
-                    // ---- land batch A in LDS, then publish readiness ----
-#define ST_LAND(g, cg, qg)                                                                             \
-        if (ST_OWN_OK(g)) {                                                                                \
-            const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + L;                   \
-            s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __uint_as_float((uint32_t)(cg)));      \
-            s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
-            s_ent[3 * e_ + 2] = oc##g;                                                                     \
-        }                                                                                                  \
-        if (!HW && (g) < hp) {                                                                             \
-            const int e_ = ST_HALO0 + L * ST_RH + ((hA + (g)) & (ST_RH - 1));                              \
-            s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __uint_as_float((uint32_t)(qg)));      \
-            s_ent[3 * e_ + 1] = hb##g;                                                                     \
-            s_ent[3 * e_ + 2] = hc##g;                                                                     \
-        }
-                    ST_LAND(0, c0, q0)
-#ifdef ST_OWNDEDUP
-                    {
-                        const float4 oa1 = dup1 ? oa0 : oa1_, ob1 = dup1 ? ob0 : ob1_, oc1 = dup1 ? oc0 : oc1_;
-                        const float4 ha1 = hdup1 ? ha0 : ha1_, hb1 = hdup1 ? hb0 : hb1_, hc1 = hdup1 ? hc0 : hc1_;
-                        ST_LAND(1, c1, q1)
-                    }
-#else
-                    ST_LAND(1, c1, q1)
-#endif
-#if ST_G_DEF > 2
-                    ST_LAND(2, c2, q2)
-                    ST_LAND(3, c3, q3)
-#endif
-#undef ST_OWN_OK
-#undef ST_GATHER
-#undef ST_ISSUE
-#undef ST_LAND
-                    lds_drain();
-                    if (L == 0 && gA) lds_st(&s_hdr[0], fB);
-                    if (hvalid && hp && !HW) lds_st(&s_halo_ready[L], hB);
-                    if (TRACE && MULTI && P.trace) {   // [2] first halo entries landed, [4] first own entries landed
-                        const bool h_now = __any(hvalid && hp > 0 && L < ST_T), o_now = gA > 0;   // b-edge streams (from J - 1)
-                        if (h_now && !tr_halo && L == 0) P.trace[8 * task + 2] = wall_clock64();
-                        if (o_now && !tr_own && L == 0) P.trace[8 * task + 4] = wall_clock64();
-                        tr_halo |= h_now;
-                        tr_own |= o_now;
-                    }
-                    const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
-#ifdef ST_STEP_PROF
-                    if (P.stats && __any(moved)) {
-                        const unsigned long long t_ = clock64();
-                        if (hp_t0) {
-                            hp_n += 1;
-                            hp_cyc += t_ - hp_t0;
-                            hp_own += (unsigned long long)gA;
-                            hp_halo += (unsigned long long)__popcll(__ballot(hp > 0)) ;
-                        }
-                        hp_t0 = t_;
-                    }
-#endif
-                    fA = fB; gA = gB; hA = hB; hcA = hcB;
-                    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
-                    q0 = m0; q1 = m1; q2 = m2; q3 = m3;
-                    if constexpr (HW) {
-                        v00 = u00; v01 = u01; v02 = u02; v10 = u10; v11 = u11; v12 = u12;
-                        wa0 = wb0; wa1 = wb1; wa2 = wb2;
-                    }
-                    if (__all(fB >= nsteps && gB == 0 && hB >= P.A)) break;
-                    if (__any(moved)) {
-                        idle = 0;
-                    } else {
-                        // back off (64..1024 cycles): hundreds of waiting tiles must not flood the
-                        // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
+                for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_hdr[1 + w]));
+                if (lds_ld(&s_abort)) break;
+                if (idle && gA == 0 && hcA == 0) {
+                    // Nothing in flight and the last round found nothing to do: wait cheaply (LDS
+                    // progress, at most one granule probe per halo lane) instead of running the
+                    // whole pipeline body on dummy loads -- idle helpers steal VALU issue slots
+                    // from the compute waves sharing their SIMD.
+                    if (__all(fA >= nsteps && hA >= P.A)) break;
+                    const int own_n = min(ST_G, min(nsteps - fA, prog + ST_RO - fA));
+                    const int halo_n = hvalid ? min(ST_G, min(P.A - hA, prog + ST_RH - hoff - 2 - hA)) : 0;
+                    bool go = own_n > 0;
+                    if (halo_n > 0)
+                        go = go || hbound ||
+                             st_granule_ready(__hip_atomic_load(hsrc + hA, __ATOMIC_RELAXED, GSCOPE), P.epoch);
+                    if (!__any(go)) {
                         ++n_hpoll;
                         if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
-                            if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 16); }
+                            if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 16); }   // 16: a helper gave up
                             break;
                         }
                         const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
@@ -1720,19 +1414,154 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         else if (idle < 16) __builtin_amdgcn_s_sleep(4);
                         else __builtin_amdgcn_s_sleep(ST_HSLEEP);
                         if (SLAB && P.tm) t_idle += wall_clock64() - ts;
+                        continue;
                     }
                 }
-            };
-            if constexpr (WIDE) {
-#ifdef ST_WIDE_NOHW
-                if (false)
+                // The batch-A loads were issued one iteration ago: wait for them once, and hand
+                // the registers back through the asm so the compiler does not track them as
+                // pending (its per-use waits would otherwise serialise the gathers below).
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(q0), "+v"(q1),
+                             "+v"(q2), "+v"(q3)::"memory");
+                // ---- stage 2: vertices for batch A ----
+                int hp = 0;   // ready prefix of the halo batch (tag == epoch; boundary planes always)
+                const bool r0 = hbound || st_granule_ready(q0, P.epoch);
+                const bool r1 = hbound || st_granule_ready(q1, P.epoch);
+                const bool r2 = hbound || st_granule_ready(q2, P.epoch);
+                const bool r3 = hbound || st_granule_ready(q3, P.epoch);
+                if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
+#define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
+#define ST_GATHER(g, cg, qg)                                                                          \
+    const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
+    const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
+    const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
+    const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
+                ST_GATHER(0, c0, q0)
+#ifdef ST_OWNDEDUP   // experiment: slot 1 repeating slot 0's label reads the shared dummy line instead
+                const bool dup1 = ST_OWN_OK(0) && ST_OWN_OK(1) && lbl_of((uint32_t)c1) == lbl_of((uint32_t)c0);
+                const bool hdup1 = 0 < hp && 1 < hp && lbl_of((uint32_t)q1) == lbl_of((uint32_t)q0);
+                const size_t so1 = 3 * SDF_CHK(11, (ST_OWN_OK(1) && !dup1 && lbl_of((uint32_t)c1) >= 0 ? lbl_of((uint32_t)c1) : gdum), 0, P.ntri);
+                const float4 oa1_ = P.soup[so1], ob1_ = P.soup[so1 + 1], oc1_ = P.soup[so1 + 2];
+                const size_t sh1 = 3 * SDF_CHK(12, (1 < hp && !hdup1 && lbl_of((uint32_t)q1) >= 0 ? lbl_of((uint32_t)q1) : gdum), 0, P.ntri);
+                const float4 ha1_ = P.soup[sh1], hb1_ = P.soup[sh1 + 1], hc1_ = P.soup[sh1 + 2];
 #else
-                if (J > 0 && K > 0)
+                ST_GATHER(1, c1, q1)
 #endif
-                    hloop(std::integral_constant<bool, true>{});
-                else hloop(std::integral_constant<bool, false>{});
-            } else {
-                hloop(std::integral_constant<bool, false>{});
+#if ST_G_DEF > 2
+                ST_GATHER(2, c2, q2)
+                ST_GATHER(3, c3, q3)
+#endif
+                // ---- stage 1: issue batch B ----
+                const int fB = fA + gA;
+                int gB = min(ST_G, min(nsteps - fB, prog + ST_RO - fB));
+                if (gB < 0) gB = 0;
+                const int hB = hA + hp;
+                int hcB = 0;
+                if (hvalid) {
+                    hcB = min(ST_G, min(P.A - hB, prog + ST_RH - hoff - 2 - hB));
+                    if (hcB < 0) hcB = 0;
+                }
+#define ST_ISSUE(g, cn, qn)                                                                            \
+    {                                                                                                  \
+        const int a_ = fB + (g) - bl - cl;                                                             \
+        const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
+        const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
+        cn = P.cell[SDF_CHK(6, ix_, P.clo, P.chi)];                                                    \
+        const unsigned long long *src_ =                                                               \
+            (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
+                       : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + hB + (g)); \
+        qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE);                                        \
+    }
+                // Always issued (a fixed count keeps the waits below precise); slots with nothing
+                // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
+                // not flood the fabric with granule polls.
+                unsigned long long n0, n1, n2, n3, m0, m1, m2, m3;
+                ST_ISSUE(0, n0, m0)
+                ST_ISSUE(1, n1, m1)
+#if ST_G_DEF > 2
+                ST_ISSUE(2, n2, m2)
+                ST_ISSUE(3, n3, m3)
+#else
+                n2 = n3 = ~0ull;
+                m2 = m3 = 0ull;
+#endif
+#ifdef ST_HALO_DELAY   // diagnostics: the first pass's sensitivity to the tile-hop latency (DESIGN.md §6)
+                if (__any(hp > 0)) __builtin_amdgcn_s_sleep(ST_HALO_DELAY);
+#endif
+                // ---- land batch A in LDS, then publish readiness ----
+#define ST_LAND(g, cg, qg)                                                                             \
+    if (ST_OWN_OK(g)) {                                                                                \
+        const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + L;                   \
+        s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __uint_as_float((uint32_t)(cg)));      \
+        s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
+        s_ent[3 * e_ + 2] = oc##g;                                                                     \
+    }                                                                                                  \
+    if ((g) < hp) {                                                                                    \
+        const int e_ = ST_HALO0 + L * ST_RH + ((hA + (g)) & (ST_RH - 1));                              \
+        s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __uint_as_float((uint32_t)(qg)));      \
+        s_ent[3 * e_ + 1] = hb##g;                                                                     \
+        s_ent[3 * e_ + 2] = hc##g;                                                                     \
+    }
+                ST_LAND(0, c0, q0)
+#ifdef ST_OWNDEDUP
+                {
+                    const float4 oa1 = dup1 ? oa0 : oa1_, ob1 = dup1 ? ob0 : ob1_, oc1 = dup1 ? oc0 : oc1_;
+                    const float4 ha1 = hdup1 ? ha0 : ha1_, hb1 = hdup1 ? hb0 : hb1_, hc1 = hdup1 ? hc0 : hc1_;
+                    ST_LAND(1, c1, q1)
+                }
+#else
+                ST_LAND(1, c1, q1)
+#endif
+#if ST_G_DEF > 2
+                ST_LAND(2, c2, q2)
+                ST_LAND(3, c3, q3)
+#endif
+#undef ST_OWN_OK
+#undef ST_GATHER
+#undef ST_ISSUE
+#undef ST_LAND
+                lds_drain();
+                if (L == 0 && gA) lds_st(&s_hdr[0], fB);
+                if (hvalid && hp) lds_st(&s_halo_ready[L], hB);
+                if (TRACE && MULTI && P.trace) {   // [2] first halo entries landed, [4] first own entries landed
+                    const bool h_now = __any(hvalid && hp > 0 && L < ST_T), o_now = gA > 0;   // b-edge streams (from J - 1)
+                    if (h_now && !tr_halo && L == 0) P.trace[8 * task + 2] = wall_clock64();
+                    if (o_now && !tr_own && L == 0) P.trace[8 * task + 4] = wall_clock64();
+                    tr_halo |= h_now;
+                    tr_own |= o_now;
+                }
+                const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
+#ifdef ST_STEP_PROF
+                if (P.stats && __any(moved)) {
+                    const unsigned long long t_ = clock64();
+                    if (hp_t0) {
+                        hp_n += 1;
+                        hp_cyc += t_ - hp_t0;
+                        hp_own += (unsigned long long)gA;
+                        hp_halo += (unsigned long long)__popcll(__ballot(hp > 0)) ;
+                    }
+                    hp_t0 = t_;
+                }
+#endif
+                fA = fB; gA = gB; hA = hB; hcA = hcB;
+                c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+                q0 = m0; q1 = m1; q2 = m2; q3 = m3;
+                if (__all(fB >= nsteps && gB == 0 && hB >= P.A)) break;
+                if (__any(moved)) {
+                    idle = 0;
+                } else {
+                    // back off (64..1024 cycles): hundreds of waiting tiles must not flood the
+                    // memory system with granule polls (MI355X_MICROARCH.md polling-cost)
+                    ++n_hpoll;
+                    if (++idle > ST_WATCHDOG || ((idle & 255u) == 0u && st_failed(P))) {
+                        if (L == 0) { lds_st(&s_abort, 1); st_fail(P, 16); }
+                        break;
+                    }
+                    const unsigned long long ts = (SLAB && P.tm) ? wall_clock64() : 0ull;
+                    if (idle < 4) __builtin_amdgcn_s_sleep(1);
+                    else if (idle < 16) __builtin_amdgcn_s_sleep(4);
+                    else __builtin_amdgcn_s_sleep(ST_HSLEEP);
+                    if (SLAB && P.tm) t_idle += wall_clock64() - ts;
+                }
             }
 #ifdef ST_STEP_PROF
             if (P.stats && L == 0) {
@@ -1803,7 +1632,6 @@ struct TileSweepWorkspace {
     int last_ntasks = 0;        // tasks of the last multi-sweep launch (watchdog report) ...
     int last_A = 0, last_B = 0, last_nJ = 0, last_ns = 0, last_nK[ST_MAXSW] = {0}, last_hbC[ST_MAXSW] = {0};
     size_t last_nhb = 0, last_nhc = 0;
-    int last_gran = 1;   // granules per halo entry of the last multi-sweep launch
 };
 
 inline bool tile_sweep_supported(int ni, int nj, int nk) { return ni >= 2 && nj >= 2 && nk >= 2; }
@@ -2085,13 +1913,8 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
         nhb = std::max(nhb, (size_t)nJ * (size_t)std::max(ce[x] - cs[x], 0) * A);
         nhc = std::max(nhc, (size_t)nKq[x] * B * A);
     }
-    // the launch's configuration (this slab's tiles per sweep, the largest sweep) decides the halo format
-    int tiles = 0;
-    for (int q = 0; q < ns; ++q) tiles = std::max(tiles, nJ * nKq[(size_t)q * nsl + me]);
-    W.cfg = st_cfg(tiles);
-    const int gran = st_halo_gran(W.cfg, nsl);   // granules per halo entry (wide entries: ST_WG)
-    nhb = std::max<size_t>(nhb * gran, 1);
-    nhc = std::max<size_t>(nhc * gran, 1);
+    nhb = std::max<size_t>(nhb, 1);
+    nhc = std::max<size_t>(nhc, 1);
     if (W.cap_mhb < ns * nhb || W.cap_mhc < ns * nhc) (void)hipStreamSynchronize(st);
     if (st_grow(&W.mhb, &W.cap_mhb, ns * nhb, st)) return fail(-5, "halo buffer allocation failed");
     if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc, st)) return fail(-5, "halo buffer allocation failed");
@@ -2293,7 +2116,6 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     W.last_ns = ns;
     W.last_nhb = nhb;
     W.last_nhc = nhc;
-    W.last_gran = gran;
     for (int q = 0; q < ns; ++q) {
         W.last_nK[q] = P.sw[q].nK;
         W.last_hbC[q] = P.sw[q].ce - P.sw[q].cs;
@@ -2301,6 +2123,10 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
     if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
+    // configuration by this slab's tiles per sweep (the largest sweep of the launch)
+    int tiles = 0;
+    for (int q = 0; q < ns; ++q) tiles = std::max(tiles, nJ * nKq[(size_t)q * nsl + me]);
+    W.cfg = st_cfg(tiles);
     if (nsl > 1) st_launch<true, false, true>(W.cfg, grid, st, P, W.lead_override);
     else if (W.trace_multi) {   // diagnostics: per-task timeline of the whole launch (tools/trace_multi.py)
         if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(-5, "trace");
@@ -2362,15 +2188,10 @@ inline void st_watchdog_report(const TileSweepWorkspace &W, const char *who)
                 task, J, K, q, eq, W.last_nJ, nK, hstep);
         auto show = [&](const char *what, const unsigned long long *base, size_t row, int a) {
             if (a < 0 || a >= A) return;   // that stream is not read at this step
-            // wide entries: the first of the entry's ST_WUSE granules, and how many carry this epoch
-            const int ng = W.last_gran > 1 ? ST_WUSE : 1;
-            unsigned long long gs[ST_WUSE] = {0};
-            if (hipMemcpy(gs, base + (row * A + a) * W.last_gran, 8 * ng, hipMemcpyDeviceToHost) != hipSuccess) return;
-            int nready = 0;
-            for (int m = 0; m < ng; ++m) nready += (unsigned)(gs[m] >> 32) == eq;
-            const unsigned long long g = gs[0];
-            fprintf(stderr, "    %-30s a = %5d: epoch %u label %d%s (%d of %d granules tagged)\n", what, a, (unsigned)(g >> 32),
-                    lbl_of((uint32_t)g), (unsigned)(g >> 32) == eq ? " (ready)" : " (NOT ready)", nready, ng);
+            unsigned long long g = 0;
+            if (hipMemcpy(&g, base + row * A + a, 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+            fprintf(stderr, "    %-30s a = %5d: epoch %u label %d%s\n", what, a, (unsigned)(g >> 32), lbl_of((uint32_t)g),
+                    (unsigned)(g >> 32) == eq ? " (ready)" : " (NOT ready)");
         };
         const unsigned long long *hb = W.mhb + (size_t)q * W.last_nhb, *hc = W.mhc + (size_t)q * W.last_nhc;
         const int b0 = J * ST_T, c0 = K * ST_T;   // one GPU: cs = 0
