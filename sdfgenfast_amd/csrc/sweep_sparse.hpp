@@ -129,6 +129,11 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                           // (second pass C3 2.95-2.97 -> 2.82-2.85 ms, C4 11.99-12.33 -> 11.85-12.18 ms,
                           // profiles/r05h_ab_repair_c{3,4}.log)
 #endif
+#ifndef SP_VMASK
+#define SP_VMASK 1   // sp_mask_w in integer VALU arithmetic instead of compare masks: Jacobi scan SALU 1.69e8 -> 0.99e8
+                     // per C4 launch; second pass C4 11.54-11.61 -> 11.40-11.42 ms, C3 neutral (profiles/r05w_ab_vmask_c{3,4}.log,
+                     // r05x_sq_{cur,vmask}_c4.log)
+#endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
@@ -263,8 +268,32 @@ __device__ __forceinline__ unsigned sp_mask_w(const SpParams &P, int i, int j, i
         lab[q] = lbl_of(w[q]);
         lcq[q] = lc_of(w[q]);
     }
-    const int ct0 = lbl_of((uint32_t)own);
     const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
+#if SP_VMASK
+    (void)live;
+    // The same test in integer VALU arithmetic (no compare masks to combine: the compare form's
+    // ~60 SGPR-mask ORs/ANDs per 64 cells made the Jacobi scan issue-bound on the CU's one scalar
+    // unit).  On raw 27-bit labels: d = min over {none, own, earlier slots} of (label ^ that) is 0
+    // exactly when the slot's label is none, the cell's own or a duplicate; bit 31 of (d | -d) is
+    // d != 0; bit 31 of (seen[q] - lc) is lc > seen[q] (both small; seen = -1: never).
+    auto opq = [](uint32_t x) { asm volatile("" : "+v"(x)); return x; };   // keeps it arithmetic
+    const uint32_t rown = (uint32_t)own & LBL_MASK;
+    const uint32_t itr = opq(interior ? 0xffffffffu : 0u);
+    uint32_t rl[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) rl[q] = w[q] & LBL_MASK;
+    unsigned f = 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        uint32_t d = min(rl[q] ^ LBL_MASK, rl[q] ^ rown);
+#pragma unroll
+        for (int r = 0; r < q; ++r) d = min(d, rl[q] ^ rl[r]);
+        d = opq(d);
+        const uint32_t keep = (d | (0u - d)) & ((uint32_t)(P.seen[q] - lcq[q]) | ~itr);
+        f |= (keep >> 31) << q;
+    }
+#else
+    const int ct0 = lbl_of((uint32_t)own);
     unsigned f = 0;   // candidates to evaluate, one bit per upwind slot q
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
@@ -275,6 +304,7 @@ __device__ __forceinline__ unsigned sp_mask_w(const SpParams &P, int i, int j, i
         skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
         f |= (skip ? 0u : 1u) << q;
     }
+#endif
 #ifdef SP_JACOBI_NOEVAL   // diagnostics only: the Jacobi pass's memory floor (wrong results)
     if (!live) f = 0;
 #endif
