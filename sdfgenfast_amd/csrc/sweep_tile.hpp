@@ -81,6 +81,10 @@ namespace sdfhip {
 #ifndef ST_QMIN
 #define ST_QMIN 1      // quad tiles: a first-minimum reduction over the quad instead of four ordered applies
 #endif
+#ifndef ST_QVMASK
+#define ST_QVMASK 1    // quad tiles: the mask's tests in integer VALU arithmetic (no compare masks to combine):
+                       // isolated step 1.141 -> 1.088 us, C3 / C4 first pass neutral (profiles/r05z_*)
+#endif
 #ifndef ST_QMASK
 #define ST_QMASK 1     // quad tiles: the candidate mask split over the cell's four lanes
 #endif
@@ -922,6 +926,24 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         const uint32_t xb = (uint32_t)st_sel4(qr, (int)raw[4], (int)raw[5], (int)raw[6], (int)raw[6]);
                         const int lb = st_sel4(qr, lcq[4], lcq[5], lcq[6], lcq[6]);
                         const int sb = st_sel4(qr, P.seen[4], P.seen[5], P.seen[6], P.seen[6]);
+#if ST_QVMASK
+                        // integer VALU form (as sweep_sparse.hpp SP_VMASK): d = min of label ^ (none, own,
+                        // earlier slots) is 0 exactly for a skipped label; bit 31 of (d | -d) is d != 0, bit
+                        // 31 of (seen - lc) is lc > seen.  The lane's "earlier slot" terms it must not test
+                        // are forced to all-ones (never 0) by per-lane masks.
+                        auto opq = [](uint32_t x) { asm volatile("" : "+v"(x)); return x; };
+                        const uint32_t m1 = qr < 1 ? ~0u : 0u, m2 = qr < 2 ? ~0u : 0u, m3 = qr < 3 ? ~0u : 0u;
+                        const uint32_t itr = opq(interior ? ~0u : 0u);
+                        uint32_t da = min(min(xa ^ LBL_MASK, xa ^ own_raw), (xa ^ raw[0]) | m1);
+                        da = min(da, min((xa ^ raw[1]) | m2, (xa ^ raw[2]) | m3));
+                        uint32_t db = min(min(xb ^ LBL_MASK, xb ^ own_raw), min(xb ^ raw[0], xb ^ raw[1]));
+                        db = min(db, min(min(xb ^ raw[2], xb ^ raw[3]), min((xb ^ raw[4]) | m1, (xb ^ raw[5]) | m2)));
+                        da = opq(da);
+                        db = opq(db);
+                        const uint32_t ka = (da | (0u - da)) & ((uint32_t)(sa - la) | ~itr);
+                        const uint32_t kb = (db | (0u - db)) & ((uint32_t)(sb - lb) | ~itr) & m3;   // (lane 3 has no slot B)
+                        unsigned bits = ((ka >> 31) << qr) | ((kb >> 31) << (qr + 4));
+#else
                         const bool keep_a = (xa != LBL_MASK) & (xa != own_raw) & !(interior & (la <= sa)) &
                                             ((qr < 1) | (xa != raw[0])) & ((qr < 2) | (xa != raw[1])) &
                                             ((qr < 3) | (xa != raw[2]));
@@ -929,6 +951,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                                             (xb != raw[0]) & (xb != raw[1]) & (xb != raw[2]) & (xb != raw[3]) &
                                             ((qr < 1) | (xb != raw[4])) & ((qr < 2) | (xb != raw[5]));
                         unsigned bits = ((keep_a ? 1u : 0u) << qr) | ((keep_b ? 1u : 0u) << (qr + 4));
+#endif
                         bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);   // quad_perm(1,0,3,2)
                         bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);   // quad_perm(2,3,0,1)
                         fmask = bits;
