@@ -1037,7 +1037,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
     int multi_n = 0;
     if (impl == 1 && ws->wf.trace_sweep < 0) {
         const char *e = getenv("SDFGEN_TILE_MULTI");
-        const int want = std::min(std::min(sparse_first, nsweeps), 8);
+        const int want = std::min(std::min(sparse_first, nsweeps), ST_MAXSW);
         const double bytes = 8.0 * want * (((nj - 1 + 7) / 8) * (double)(nk - 1) + ((nk - 1 + 7) / 8) * (double)(nj - 1)) *
                              (double)(ni - 1);
         size_t free_b = 0, total_b = 0;

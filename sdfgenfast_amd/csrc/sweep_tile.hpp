@@ -209,7 +209,11 @@ __device__ __forceinline__ unsigned long long st_granule(unsigned epoch, uint32_
 __device__ __forceinline__ bool st_granule_ready(unsigned long long g, unsigned epoch) { return (uint32_t)(g >> 32) == epoch; }
 
 // Per-sweep fields of one launch that runs several sweeps (MULTI, see k_sweep_tile).
-constexpr int ST_MAXSW = 8;
+#ifndef ST_MAXSW_DEF
+#define ST_MAXSW_DEF 8
+#endif
+constexpr int ST_MAXSW = ST_MAXSW_DEF;   // sweeps one multi-sweep launch can hold (a power of two)
+static_assert((ST_MAXSW & (ST_MAXSW - 1)) == 0, "sweep slots: a power of two");
 constexpr int ST_MAXDEP = 16;   // previous-sweep tiles a tile depends on (3x3 with margins)
 struct StSweep {
     unsigned long long *hb, *hc;  // this sweep's halo granule buffers
