@@ -24,18 +24,18 @@ uncached system-scope round trip is 0.82 us, tools/uc_lat).
 """
 import json
 
-# ---- measured inputs (one MI355X, round 4) ----
+# ---- measured inputs (one MI355X, round 5) ----
 INPUTS = {
-    "c3_sphere1m_256": {   # bench r04v (final round-4 build 282f81e0): 14.14 ms total; tile launch 10.32 ms; 8 sparse sweeps 2.95 ms
-        "dims": (256, 256, 256), "t_local": 0.8616, "t_first": 10.322, "t_second": 2.9534,
-        "t_repair_per_sweep": 0.240,   # k_sp_recheck per sweep at C3 (r04v kernel stats, mean of 8 x 6 calls)
+    "c3_sphere1m_256": {   # bench r05y (build 9e941c33): 13.71 ms in phases; tile launch 10.23 ms; 8 sparse sweeps 2.72 ms
+        "dims": (256, 256, 256), "t_local": 0.7504, "t_first": 10.2276, "t_second": 2.7227,
+        "t_repair_per_sweep": 0.2116,  # k_sp_recheck per sweep at C3 (profiles/r05y_c3_kernel_stats.csv, 8 x 6 calls)
         "t_first_work": 5.0,           # tile work at full throughput: C4's first pass x 1/8 of the cells
         "longest_chain": 86,           # longest relabel chain of a second-pass sweep (oracle)
     },
-    "c4_sphere1m_512": {   # bench r04v zslab_c4 side object: 54.31 ms; tile 39.88 ms; sparse 12.34 ms
-        "dims": (512, 512, 512), "t_local": 1.9756, "t_first": 39.882, "t_second": 12.342,
+    "c4_sphere1m_512": {   # round 5 A/B (profiles/r05w_ab_vmask_c4.log): 53.7 ms; tile 40.15 ms; sparse 11.40 ms
+        "dims": (512, 512, 512), "t_local": 2.15, "t_first": 40.15, "t_second": 11.40,
         "t_repair_per_sweep": 0.62,    # repair_ms per sweep, 2-slab rehearsal (r03c_n2 zslab_c4), median
-        "t_first_work": 39.882,        # throughput-bound at one GPU: the launch itself
+        "t_first_work": 40.15,         # throughput-bound at one GPU: the launch itself
         "longest_chain": 172,          # not measured at C4: 2 x C3's (chains scale with the grid edge)
         # round 5, one MI355X (profiles/r05d_sparse_from_c4.log, SDFGEN_SPARSE_FROM=k, per-sweep events): the
         # first pass's last sweeps as Jacobi + repair instead of inside the tile launch -- the tile launch of the
@@ -45,7 +45,7 @@ INPUTS = {
                         6: {"tile": 32.296, "sparse_first": [30.297, 37.807]}},
     },
 }
-S_ISO_US = 1.1649    # isolated tile step, quad-lane tiles (bench r04v latency probe, 1024x9x9 grid)
+S_ISO_US = 1.088     # isolated tile step, quad-lane tiles (round 5 latency probe, 1024x9x9 grid: profiles/r05z_steplat_qvm.log)
 H_X_US = 2.0         # cross-GPU granule hand-off over xGMI (assumed; on-chip uncached round trip 0.82 us)
 H_FLAG_US = 2.0      # one DONE / READY flag hand-off between neighbour GPUs (assumed, as h_x)
 LINK_IDLE_US = 1.25  # one repair chain link on an idle chip: ~4 returning atomics + 2 dependent loads, ~3,000 cycles
