@@ -81,6 +81,10 @@ namespace sdfhip {
 #ifndef ST_QMIN
 #define ST_QMIN 1      // quad tiles: a first-minimum reduction over the quad instead of four ordered applies
 #endif
+#ifndef ST_GVMASK
+#define ST_GVMASK 1    // 1-wave and twin-lane tiles: the same integer VALU form of the candidate mask: C4 first pass
+                       // (1-wave tiles, throughput-bound) 40.10-40.15 -> 39.04-39.13 ms (profiles/r05ac_*)
+#endif
 #ifndef ST_QVMASK
 #define ST_QVMASK 1    // quad tiles: the mask's tests in integer VALU arithmetic (no compare masks to combine):
                        // isolated step 1.141 -> 1.088 us, C3 / C4 first pass neutral (profiles/r05z_*)
@@ -983,6 +987,21 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         bits |= (unsigned)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);   // quad_perm(1,0,3,2)
                         fmask = bits;
                     } else {
+#if ST_GVMASK
+                    // integer VALU form of the test below (as ST_QVMASK / sweep_sparse.hpp SP_VMASK)
+                    auto opq = [](uint32_t x) { asm volatile("" : "+v"(x)); return x; };
+                    const uint32_t own_raw = own_w & LBL_MASK, itr = opq(interior ? ~0u : 0u);
+#pragma unroll
+                    for (int q = 0; q < 7; ++q) {
+                        const uint32_t x = (uint32_t)lab[q];
+                        uint32_t d = min(x ^ LBL_MASK, x ^ own_raw);
+#pragma unroll
+                        for (int r = 0; r < q; ++r) d = min(d, x ^ (uint32_t)lab[r]);
+                        d = opq(d);
+                        const uint32_t keep = (d | (0u - d)) & ((uint32_t)(P.seen[q] - lcq[q]) | ~itr);
+                        fmask |= (keep >> 31) << q;
+                    }
+#else
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {   // bitwise, no short-circuit branches
                         bool skip = (lab[q] == (int)LBL_MASK) | (lab[q] == (int)(own_w & LBL_MASK));   // none, or the own label
@@ -991,6 +1010,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         skip = skip | (interior & (lcq[q] <= P.seen[q]));   // seen[q] = -1: never
                         fmask |= (skip ? 0u : 1u) << q;
                     }
+#endif
                     }
                 }
 #ifdef ST_LDS_PROBE   // diagnostics: a dependent chain of N extra LDS reads per compute step
