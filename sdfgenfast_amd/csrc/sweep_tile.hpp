@@ -83,7 +83,8 @@ namespace sdfhip {
 #endif
 #ifndef ST_GVMASK
 #define ST_GVMASK 1    // 1-wave and twin-lane tiles: the same integer VALU form of the candidate mask: C4 first pass
-                       // (1-wave tiles, throughput-bound) 40.10-40.15 -> 39.04-39.13 ms (profiles/r05ac_*)
+                       // (1-wave tiles, throughput-bound) 40.10-40.15 -> 39.04-39.13 ms (profiles/r05ac_*); with the apply
+                       // reading non-candidates as +inf 38.77-38.80 ms (r05ad_*)
 #endif
 #ifndef ST_QVMASK
 #define ST_QVMASK 1    // quad tiles: the mask's tests in integer VALU arithmetic (no compare masks to combine):
@@ -1299,8 +1300,17 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     for (int q = 0; q < 7; ++q) dq[q] = __int_as_float(s_pd[w][7 * ST_CPW + q * ST_CPW + L]);
 #pragma unroll
                     for (int q = 0; q < 7; ++q) {
+#if ST_GVMASK
+                        // a slot that is not a candidate reads as +inf, which never passes '<' (one compare,
+                        // no mask to combine on the scalar unit)
+                        const uint32_t cm = 0u - ((fmask >> q) & 1u);
+                        const float dv = __uint_as_float((__float_as_uint(dq[q]) & cm) | (0x7f800000u & ~cm));
+                        const bool take = dv < phi;
+#else
                         const bool take = ((fmask >> q) & 1u) && dq[q] < phi;
-                        phi = take ? dq[q] : phi;
+                        const float dv = dq[q];
+#endif
+                        phi = take ? dv : phi;
                         ct = take ? lab[q] : ct;
                         win = take ? ent[q] : win;
                     }
