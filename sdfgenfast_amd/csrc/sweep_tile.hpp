@@ -134,7 +134,12 @@ struct StCfg {
     // Ring slots: a column's entry for a is last read 3 steps after it is written (as the a - 1
     // neighbour of the diagonal column), so one compute wave needs 4; several need 4 more for the
     // lead between them (RR = 4 with 2 waves measured wrong results: no lead left).
-    static_assert((RR & (RR - 1)) == 0 && (RR >= 8 || (NCW == 1 && RR == 4)), "ring slots: power of two, >= 8 (4 with one compute wave)");
+    // One compute wave reads a step's neighbours before it writes the step back, so 3 slots are enough
+    // there (the entry written at step h is read last at step h + 3, before that step's write-back into
+    // the same slot); 3 is not a power of two: slots by a modulo (RR_POW2 below).
+    static_assert(((RR & (RR - 1)) == 0 && (RR >= 8 || (NCW == 1 && RR == 4))) || (NCW == 1 && RR == 3 && LPC == 1),
+                  "ring slots: power of two, >= 8 (4 or 3 with one compute wave)");
+    static constexpr bool RR_POW2 = (RR & (RR - 1)) == 0;
 };
 // Round 3's latency-bound tiles (SDFGEN_TILE_CFG=0 only since round 4): 2 compute waves of 32 cells
 // with twin lanes; ~47 KB LDS, 3 tiles per CU.  Throughput-bound grids (C4, C5): ONE
@@ -144,7 +149,10 @@ using StCfgLat = StCfg<ST_NCW_DEF, ST_RR_DEF, (ST_TWIN != 0), ST_WPE_DEF>;
 #ifndef ST_THR_WPE
 #define ST_THR_WPE 2
 #endif
-using StCfgThr = StCfg<1, 4, false, ST_THR_WPE>;
+#ifndef ST_THR_RR
+#define ST_THR_RR 4
+#endif
+using StCfgThr = StCfg<1, ST_THR_RR, false, ST_THR_WPE>;
 // Latency-bound grids, quad lanes: 4 compute waves of 16 cells, four lanes per cell -- every step
 // evaluates up to 4 candidates per cell in ONE pass (lane 4x + r takes the cell's r-th candidate in
 // check order) and a first-minimum reduction over the quad combines them, so no step pays the
@@ -642,6 +650,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 sp_t = clock64();
 #endif
                 const int a = h - bl - cl;
+                // ring slot of a and of a - 1 (RR = 3: a modulo; a > -2^20 here)
+                const int am = Cfg::RR_POW2 ? (a & (ST_RR - 1)) : (int)((unsigned)(a + 3 * (1 << 20)) % (unsigned)ST_RR);
+                const int amm = Cfg::RR_POW2 ? ((a - 1) & (ST_RR - 1)) : (am == 0 ? ST_RR - 1 : am - 1);
                 const bool act = col && a >= 0 && a < P.A;
                 const bool actx = ((TWIN || Cfg::QUAD) ? colx : col) && a >= 0 && a < P.A;   // the lanes that evaluate
                 // ---- wait for: own data + halo (helper), wave w-1's step h-1, ring space in w+1 ----
@@ -911,6 +922,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                         const int aq = (q & 1) == 0 ? a - 1 : a;   // q = 0,2,4,6 read a-1
                         if constexpr (EB)
                             ent[q] = (nb_base[q] & 0xffff) + (((q & 1) == 0 ? t48m : t48a) << (nb_base[q] >> 16));
+                        else if constexpr (!Cfg::RR_POW2)   // ring entries (shift 6) by slot, halo entries by mask
+                            ent[q] = nb_base[q] + ((nb_sh[q] == 6 ? ((q & 1) == 0 ? amm : am) : (aq & nb_mask[q])) << nb_sh[q]);
                         else
                             ent[q] = nb_base[q] + ((aq & nb_mask[q]) << nb_sh[q]);
                         const uint32_t wq = __float_as_uint(st_e<EB>(s_ent, ent[q], 0).w);
@@ -1324,7 +1337,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     const int src = win < 0 ? e_own : win;
                     const float4 w0 = st_e<EB>(s_ent, src, 0);
                     const float4 w1 = st_e<EB>(s_ent, src, 1), w2 = st_e<EB>(s_ent, src, 2);
-                    const int slot = __umul24(ST_RING0 + (a & (ST_RR - 1)) * ST_NCOL + col_id, ES);
+                    const int slot = __umul24(ST_RING0 + am * ST_NCOL + col_id, ES);
                     // a winner always carries a new label (the own label is never a candidate); quad
                     // tiles (ST_QMIN) take it from the winner's entry, the word its candidate test read
                     const uint32_t w_new = win < 0 ? own_w
