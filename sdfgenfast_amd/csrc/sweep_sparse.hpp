@@ -134,6 +134,10 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                      // per C4 launch; second pass C4 11.54-11.61 -> 11.40-11.42 ms, C3 neutral (profiles/r05w_ab_vmask_c{3,4}.log,
                      // r05x_sq_{cur,vmask}_c4.log)
 #endif
+#ifndef SP_JSCAN_FAST
+#define SP_JSCAN_FAST 1   // k_sp_jacobi on one device below 2^29 cells: scalar neighbour bases, one 32-bit offset, and
+                          // only "any candidate" (sp_any_scan) -- the scan is VALU-issue-bound since SP_VMASK
+#endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
@@ -309,6 +313,27 @@ __device__ __forceinline__ unsigned sp_mask_w(const SpParams &P, int i, int j, i
     if (!live) f = 0;
 #endif
     return f;
+}
+
+// Whether sp_mask_w's mask is non-zero, for the Jacobi scan's list decision (which needs nothing more):
+// the same tests on the raw words, with the keep bit formed as ~(d - 1) (d < 2^27, so bit 31 of d - 1 is
+// d == 0) and the seven keep words OR-ed together instead of packed into a mask -- 83 instead of ~105
+// VALU per cell.
+__device__ __forceinline__ bool sp_any_scan(const SpParams &P, uint32_t own, const uint32_t (&w)[7], bool interior)
+{
+    auto opq = [](uint32_t x) { asm volatile("" : "+v"(x)); return x; };   // keeps it arithmetic (sp_mask_w)
+    const uint32_t itr = opq(interior ? 0xffffffffu : 0u);
+    uint32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+        uint32_t d = min((w[q] ^ LBL_MASK) & LBL_MASK, (w[q] ^ own) & LBL_MASK);
+#pragma unroll
+        for (int r = 0; r < q; ++r) d = min(d, (w[q] ^ w[r]) & LBL_MASK);
+        d = opq(d);
+        const uint32_t sq = (uint32_t)(P.seen[q] - (int)(w[q] >> LBL_BITS));   // bit 31: lc > seen[q]
+        acc |= ~(d - 1u) & (sq | ~itr);
+    }
+    return (acc >> 31) != 0u;
 }
 
 template <bool LIVE, bool SLAB = false>
@@ -666,19 +691,30 @@ __device__ __forceinline__ void sp_jlist_flush(const SpParams &P, unsigned part,
     sp_wave_sync();
 }
 
-template <bool SLAB>
+// FAST (one device, c_lo = 0, n <= 2^29 so that byte offsets fit 32 bits): the same traversal, with
+//   * the cell and its 7 upwind words loaded with ONE 32-bit byte offset from eight scalar bases (the
+//     neighbours' displacements folded into the bases: no address arithmetic per neighbour; a base
+//     may point outside the grid, but only cells inside the sweep's range -- whose upwind neighbours
+//     all exist -- load through it);
+//   * the mask reduced to sp_any_scan (the list decision needs no more).
+// 178 -> ~130 VALU per 64 cells: C3 scan 89.5 -> 76.2 us, C4 639 -> 629 us (profiles/r05aq_jscan_kernel_stats.txt).
+// C4's scan sat at 95 % VALU issue (SQ) and is no faster with fewer VALU, nor with the next cell's loads
+// issued before this cell's mask (75 % VALU issue then), nor in a (j, k, i) plane-range order (which
+// slowed the list pass: its cells lost their address order).
+template <bool SLAB, bool FAST = false>
 __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 {
+    static_assert(!(SLAB && FAST), "the fast scan is for one device");
     __shared__ unsigned s_list[4][SP_JWAVE];
+    const unsigned lane = threadIdx.x & 63;
+    const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD
+    unsigned *buf = s_list[threadIdx.x >> 6];
+    unsigned cnt = 0;   // wave-uniform
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs, so XCD x walks the x-th
     // contiguous eighth of the grid -- the neighbour planes a cell reads sit in its own L2.
     const bool xcd = gridDim.x % 8 == 0;
     const unsigned long long span = xcd ? (P.n + 7) / 8 : P.n;
     const unsigned long long base = xcd ? (unsigned long long)(blockIdx.x % 8) * span : 0ull;
-    const unsigned lane = threadIdx.x & 63;
-    const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD
-    unsigned *buf = s_list[threadIdx.x >> 6];
-    unsigned cnt = 0;   // wave-uniform
 #if SP_JACOBI_CHUNK
     // Each block scans one contiguous chunk of its XCD's eighth, so blocks are dispatched in
     // address order and the upwind plane a cell reads was just read by the blocks before it: still
@@ -708,12 +744,38 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
         sj = (int)(rs % (unsigned)P.nj);
         sk = (int)(rs / (unsigned)P.nj);
     }
+    const char *nbase[7];   // FAST: the 7 upwind words' scalar bases
+    long long off[7];
+    if (FAST) {
+        const long long di = P.di, dj = (long long)P.dj * P.ni, dk = (long long)P.dk * P.ni * P.nj;
+        off[0] = -di; off[1] = -dj; off[2] = -di - dj; off[3] = -dk; off[4] = -di - dk; off[5] = -dj - dk;
+        off[6] = -di - dj - dk;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) nbase[q] = (const char *)(P.S + off[q]);   // (global pointers: no FLAT)
+    }
     for (unsigned long long it = first; it - lane < c_end; it += step) {   // wave-uniform trip count
         const bool valid = it < c_end && base + it < P.n;
         const unsigned long long c = P.c_lo + base + it;
         const unsigned c32 = (unsigned)c;   // cells < 2^32 (sparse_sweep_supported)
         unsigned f = 0;
-        if (valid) {
+        if (FAST && valid) {
+            const uint32_t boff = c32 << 3;   // < 2^32 (c < 2^29)
+            (void)SDF_CHK(20, c, 0, P.n);
+            const unsigned long long s = *(const unsigned long long *)((const char *)P.S + boff);
+            if (sp_in(P, i, j, k)) {
+                uint32_t w[7];
+                uint32_t bo = boff;
+                asm volatile("" : "+v"(bo));   // zero-extended in this block: the loads take the scalar-base form
+#pragma unroll
+                for (int q = 0; q < 7; ++q) {
+                    (void)SDF_CHK(22, (unsigned long long)((long long)c + off[q]), 0, P.n);
+                    w[q] = *(const uint32_t *)(nbase[q] + bo);
+                }
+                const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
+                f = sp_any_scan(P, (uint32_t)s, w, interior) ? 1u : 0u;
+            }
+            if (!f && !P.sv) P.X[c] = s;   // (in place the cell already holds it)
+        } else if (valid) {
             const unsigned long long s = P.S[c];
             int lab[7];
             if (sp_in(P, i, j, k)) f = sp_mask<false, SLAB>(P, P.S, i, j, k, c, s, lab);
@@ -1640,6 +1702,16 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     return 0;
 }
 
+// the one-device scan, in its fast form where the byte offsets fit 32 bits
+inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const SpParams &P)
+{
+    if (SP_JSCAN_FAST && P.c_lo == 0 && P.n == (unsigned long long)P.ni * P.nj * P.nk && P.k_lo == 0 && P.k_hi == P.nk &&
+        P.n <= (1ull << 29) && blocks % 8 == 0)
+        hipLaunchKernelGGL((k_sp_jacobi<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+    else
+        hipLaunchKernelGGL((k_sp_jacobi<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+}
+
 // Enqueue one sparse sweep on `st`: reads *cell, writes the other buffer, then swaps
 // the two so *cell holds the result.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long **cell,
@@ -1664,7 +1736,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         if (sp_grow(&W.bbits, &W.cap_bbits, B.nbricks * SPB_WORDS, true, st)) return -5;
         B.breq = W.breq;
         B.bits = W.bbits;
-        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        sp_launch_jacobi(blocks, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
         hipLaunchKernelGGL(k_sp_jlist_brick, dim3(32 * SP_JPARTS), dim3(256), 0, st, P, B);
         if (hipGetLastError() != hipSuccess) return -4;
@@ -1675,7 +1747,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         P.S = *cell;
         P.X = *cell;
         P.sv = W.alt;
-        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        sp_launch_jacobi(blocks, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
         hipLaunchKernelGGL(k_sp_jlist<false>, dim3(32 * SP_JPARTS), dim3(256), 0, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
@@ -1685,7 +1757,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
     } else {
         P.S = *cell;
         P.X = W.alt;
-        hipLaunchKernelGGL(k_sp_jacobi<false>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        sp_launch_jacobi(blocks, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
         const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
         hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);

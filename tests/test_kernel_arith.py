@@ -7,6 +7,8 @@ parity suites.
     d = min over {none, own, earlier slots} of (label ^ that); keep = bit 31 of (d | -d) and of
     (seen - lc) | ~interior -- against sweep_sparse.hpp's compare form;
   * the quad tiles' per-lane split of the same test (ST_QVMASK: lane r decides slots r and r + 4);
+  * the Jacobi scan's list decision (sweep_sparse.hpp sp_any_scan): the seven keep words
+    ~(d - 1) & ((seen - lc) | ~interior) OR-ed together, bit 31 = "the mask is non-zero";
   * the band's box coordinates by float reciprocal plus one correction (sdfgen_hip.hip BAND_FDIV);
   * the band's wave-wide search for a pair's triangle (sdfgen_hip.hip band_wq) against find_q.
 """
@@ -90,6 +92,21 @@ def _mask_quad(w, seen, interior):
     return f
 
 
+def _any_scan(w, seen, interior):
+    """sp_any_scan: on the raw words, d from (x ^ y) & LBL_MASK, keep = ~(d - 1) & (s | ~itr), OR over q."""
+    M = U32(LBL_MASK)
+    itr = np.where(interior, U32(0xFFFFFFFF), U32(0)).astype(U32)
+    acc = np.zeros(len(w), U32)
+    for q in range(7):
+        x = w[:, q]
+        d = np.minimum((x ^ M) & M, (x ^ w[:, 7]) & M)
+        for r in range(q):
+            d = np.minimum(d, (x ^ w[:, r]) & M)
+        s = (np.int64(seen[q]) - (x >> U32(LBL_BITS)).astype(np.int64)).astype(U32)
+        acc |= ~(d - U32(1)) & (s | ~itr)
+    return (acc >> U32(31)).astype(bool)
+
+
 @pytest.mark.parametrize("seed", [1, 2, 3])
 def test_candidate_mask_integer_form_equals_compare_form(seed):
     rng = np.random.default_rng(seed)
@@ -99,6 +116,7 @@ def test_candidate_mask_integer_form_equals_compare_form(seed):
         ref = _mask_compare(w, seen, interior)
         assert np.array_equal(_mask_arith(w, seen, interior), ref)
         assert np.array_equal(_mask_quad(w, seen, interior), ref)
+        assert np.array_equal(_any_scan(w, seen, interior), ref != 0)
 
 
 def test_band_float_reciprocal_division_is_exact():
