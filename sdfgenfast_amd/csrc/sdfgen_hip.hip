@@ -154,7 +154,7 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 #define BAND_BT_DEF 64   // 64 (with the 40 KB table): band 0.86 -> 0.81 ms at C3; 16: 0.99
 #endif
 #ifndef BAND_LDS_DEF
-#define BAND_LDS_DEF 5120
+#define BAND_LDS_DEF 4000   // 31 KB: with BAND_WPE 4, four workgroups per CU (5120, 40 KB: three)
 #endif
 #ifndef BAND_FDIV
 #define BAND_FDIV 1      // box coordinates by float reciprocal + one exact correction: band 0.797 -> 0.765 ms at C3
@@ -166,7 +166,7 @@ __device__ __forceinline__ size_t cidx(int i, int j, int k, int ni, int nj)
 // evaluation), BAND_DIAG_NOFLUSH (no global atomics from the LDS table), BAND_DIAG_NOPAIR (no pairs:
 // the batches' set-up, ray parity, table initialisation and barriers)
 constexpr int BAND_BT = BAND_BT_DEF;    // triangles per batch (<= 64: one wave sets a batch up)
-constexpr int BAND_LDS = BAND_LDS_DEF;  // u64 keys in the LDS table (40 KB)
+constexpr int BAND_LDS = BAND_LDS_DEF;  // u64 keys in the LDS table (31 KB)
 static_assert(BAND_BT >= 1 && BAND_BT <= 64, "a batch's boxes are scanned by one wave");
 // find_q's binary search halves from BAND_BT / 2: it reaches every triangle only for a power of two
 // (BAND_BT_DEF=48 measured a digest mismatch at C3: triangle 47 of a batch was never paired)
@@ -275,7 +275,13 @@ __device__ __forceinline__ int band_wq(unsigned pl, unsigned F, unsigned lane)
     return q;
 }
 
-__global__ void __launch_bounds__(256) k_band_lds(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
+#ifndef BAND_WPE
+#define BAND_WPE 4   // waves per SIMD the band kernel's register budget must allow: 128 VGPRs (166 unbounded; the
+                     // spills stay in the batch set-up) and, with the 31 KB table, 4 workgroups per CU instead of 3:
+                     // band C3 0.662 -> 0.629-0.635 ms, C4 1.18-1.19 -> 1.17-1.18 (profiles/r05aw_ab_band_c{3,4}.log);
+                     // 5 waves (96 VGPRs) spill inside the pair loop
+#endif
+__global__ void __launch_bounds__(256, BAND_WPE) k_band_lds(const float4 *__restrict__ soup, uint64_t ntri, Grid g, int band,
                                                   float init, u64 *__restrict__ cell, uint32_t *__restrict__ cnt,
                                                   unsigned long long *__restrict__ eval_count, int k_lo, int k_hi,
                                                   BandBig big)
