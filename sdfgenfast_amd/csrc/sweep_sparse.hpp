@@ -134,6 +134,9 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                      // per C4 launch; second pass C4 11.54-11.61 -> 11.40-11.42 ms, C3 neutral (profiles/r05w_ab_vmask_c{3,4}.log,
                      // r05x_sq_{cur,vmask}_c4.log)
 #endif
+#ifndef SP_JBLOCKS
+#define SP_JBLOCKS 16384   // most 256-thread workgroups of the Jacobi scan (a multiple of 8 XCDs x SP_JPARTS)
+#endif
 #ifndef SP_JSCAN_FAST
 #define SP_JSCAN_FAST 1   // k_sp_jacobi on one device below 2^29 cells: scalar neighbour bases, one 32-bit offset, and
                           // only "any candidate" (sp_any_scan) -- the scan is VALU-issue-bound since SP_VMASK
@@ -1617,6 +1620,18 @@ inline int sp_grow(T **p, size_t *cap, size_t need, bool zero, hipStream_t st)
     return 0;
 }
 
+// Workgroups of the Jacobi scan over n cells: about 8 cells per thread (a workgroup's set-up and list flush
+// amortised: C3 scan 76.5 -> 71.2 us per sweep against 4 cells per thread, profiles/r05ba_jblocks.txt), but
+// at least one round of the chip's 2,048 resident workgroups, at most SP_JBLOCKS (C4: 32 cells per thread,
+// as fast as 16, faster than 64), and a multiple of the 8 XCDs (k_sp_jacobi's traversal).
+inline unsigned long long sp_jblocks(unsigned long long n)
+{
+    unsigned long long b = std::max<unsigned long long>((n + 2047) / 2048, 2048);
+    b = std::min<unsigned long long>(b, (n + 255) / 256);
+    b = std::min<unsigned long long>(b, SP_JBLOCKS);
+    return (b + 7) / 8 * 8;
+}
+
 // Workspace for sparse sweeps over n cells (allocations only: a Z-slab grows it before it
 // enqueues anything, since a later hipFree would synchronise the device mid-call).
 inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, hipStream_t st)
@@ -1628,9 +1643,7 @@ inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, hipStream_t
         if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
         if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
     }
-    unsigned long long blocks = (n + 255) / 256;
-    if (blocks > 16384) blocks = 16384;
-    blocks = (blocks + 7) / 8 * 8;
+    const unsigned long long blocks = sp_jblocks(n);
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
     const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
     if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
@@ -1654,9 +1667,7 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     // per sweep: reset the list counters; error bits and statistics accumulate over the call
     if (zero_async(W.ctl + SP_QUEUE, (SP_DIAGX - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
         return -4;
-    blocks = (n + 255) / 256;
-    if (blocks > 16384) blocks = 16384;
-    blocks = (blocks + 7) / 8 * 8;   // a multiple of the 8 XCDs (k_sp_jacobi's traversal)
+    blocks = sp_jblocks(n);
     // each list part holds every cell its blocks visit (~n/64), so it never overflows; sizing
     // it for the ~10 % that are listed would need an in-place fallback whose registers
     // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it

@@ -7,7 +7,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=$1; shift
-cfgs=(); for v in "$@"; do cfgs+=("SDFGEN_LIB_OVERRIDE=ab/$v.so"); done
+lib() { [ "$1" = cur ] && echo "" || echo "ab/$1.so"; }   # "cur": the in-tree library
+cfgs=(); for v in "$@"; do cfgs+=("SDFGEN_LIB_OVERRIDE=$(lib $v)"); done
 for v in "$@"; do
   [ "$v" = cur ] && continue
   SDFGEN_LIB_OVERRIDE=ab/$v.so timeout -k 10 600 python3 -u -m pytest tests/test_gpu_tile_cfg.py tests/test_gpu_parity.py -m gpu -q -x \
@@ -21,6 +22,6 @@ for w in c3_sphere1m_256 c4_sphere1m_512; do
   if [ $rc -ge 124 ]; then exit $rc; fi
 done
 for v in "$@"; do
-  SDFGEN_LIB_OVERRIDE=ab/$v.so timeout -k 10 300 python3 tools/step_lat.py 2 > gpurun_out/${TAG}_steplat_$v.log 2>&1
+  SDFGEN_LIB_OVERRIDE=$(lib $v) timeout -k 10 300 python3 tools/step_lat.py 2 > gpurun_out/${TAG}_steplat_$v.log 2>&1
   echo "step $v: $(tr '\n' ' ' < gpurun_out/${TAG}_steplat_$v.log)"
 done
