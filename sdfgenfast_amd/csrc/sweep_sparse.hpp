@@ -134,6 +134,10 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                      // per C4 launch; second pass C4 11.54-11.61 -> 11.40-11.42 ms, C3 neutral (profiles/r05w_ab_vmask_c{3,4}.log,
                      // r05x_sq_{cur,vmask}_c4.log)
 #endif
+#ifndef SP_JLIST_PER_PART
+#define SP_JLIST_PER_PART 128  // list-pass workgroups per Jacobi list part (one device): 32 -> 128, C4 list pass 282 -> 262 us per
+                               // sweep, C3 39.5 -> 38 us (profiles/r05bd_jlist_grid.txt; 256 the same, 512 slower)
+#endif
 #ifndef SP_JBLOCKS
 #define SP_JBLOCKS 16384   // most 256-thread workgroups of the Jacobi scan (a multiple of 8 XCDs x SP_JPARTS)
 #endif
@@ -1760,7 +1764,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         P.sv = W.alt;
         sp_launch_jacobi(blocks, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
-        hipLaunchKernelGGL(k_sp_jlist<false>, dim3(32 * SP_JPARTS), dim3(256), 0, st, P);
+        hipLaunchKernelGGL(k_sp_jlist<false>, dim3(SP_JLIST_PER_PART * SP_JPARTS), dim3(256), 0, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
         hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
@@ -1770,7 +1774,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         P.X = W.alt;
         sp_launch_jacobi(blocks, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
-        const unsigned long long lblocks = 32 * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
+        const unsigned long long lblocks = SP_JLIST_PER_PART * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
         hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
         if (hipGetLastError() != hipSuccess) return -4;
         hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
