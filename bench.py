@@ -417,27 +417,25 @@ def main():
     ndev = max(_lib.device_count(), 1)
     dev = local_rank % ndev   # = local_rank on a node with a GPU per rank
     shared = world > ndev     # a rehearsal with several slabs per GPU (one-GPU box)
-    if shared and "SDFGEN_TILE_GRID" not in os.environ:
-        # Co-resident slabs: the persistent first-pass grids must fit on the one GPU together
-        # (3 tile workgroups per CU), or a waiting slab can hold every CU its upstream slab needs.
-        os.environ["SDFGEN_TILE_GRID"] = str(max(32, 3 * 256 // ((world + ndev - 1) // ndev) - 32))
-    if shared and "SDFGEN_SPARSE_WORKERS" not in os.environ:
-        # ... and so must the slabs' repair kernels (each ends only after its upstream neighbour's): the
-        # chip holds 2,048 of their one-wave workgroups (171 VGPRs), the default is 256 per slab
-        os.environ["SDFGEN_SPARSE_WORKERS"] = str(max(32, 1024 // ((world + ndev - 1) // ndev)))
+    if shared and "SDFGEN_SLABS_PER_DEVICE" not in os.environ:
+        # Co-resident slabs of several processes: the library caps each slab's persistent grids (first
+        # pass and repair) from the occupancy query and the slab count per device; it counts its own
+        # process's sessions, so ranks sharing a GPU tell it how many share (sdfgen_hip.hip slab_share)
+        os.environ["SDFGEN_SLABS_PER_DEVICE"] = str((world + ndev - 1) // ndev)
     _hiprt.set_device(dev)
     topo = None
     if world > 1:
         # which GPU each rank drives (device, PCI bus id) and the node's peer-access matrix, so that a
         # mapping failure or watchdog on a multi-GPU node can be tied to the rank pair (the library's
         # slab errors name slab, device and PCI id of both sides)
-        t = _lib.topology()
+        # (an A/B library built before ABI 4 has no sdfgen_hip_topology: the line records null then)
+        t = _lib.topology() if hasattr(_lib.lib, "sdfgen_hip_topology") else None
         me = {"rank": rank, "local_rank": local_rank, "device": dev, "host": socket.gethostname(),
-              "pci_bus_id": t["pci_bus_ids"][dev] if dev < len(t["pci_bus_ids"]) else None}
+              "pci_bus_id": t["pci_bus_ids"][dev] if t and dev < len(t["pci_bus_ids"]) else None}
         ranks = [None] * world
         dist.all_gather_object(ranks, me)
-        topo = {"ranks": ranks, "devices": t["devices"], "pci_bus_ids": t["pci_bus_ids"],
-                "peer_access": t["peer_access"]}
+        topo = None if t is None else {"ranks": ranks, "devices": t["devices"], "pci_bus_ids": t["pci_bus_ids"],
+                                       "peer_access": t["peer_access"]}
     step_us = step_latency(dev) if rank == 0 and not args.no_latency else None
 
     res_side = {}

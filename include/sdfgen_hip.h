@@ -36,7 +36,8 @@ extern "C" {
 /* The library is built with -fvisibility=hidden: exactly what this header declares is exported. */
 #pragma GCC visibility push(default)
 
-#define SDFGEN_HIP_ABI_VERSION 4   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers, tile_cfg; 4: sdfgen_hip_topology */
+#define SDFGEN_HIP_ABI_VERSION 5   /* 2: sdfgen_hip_profile.slabs / chain_steps, slab_prepare; 3: slab_* phase timers, tile_cfg; 4: sdfgen_hip_topology;
+                                      5: sdfgen_hip_slab_close_imports (release keeps IPC mappings) */
 
 enum {
     SDFGEN_HIP_OK = 0,
@@ -156,10 +157,10 @@ typedef struct sdfgen_hip_profile {
 
 int sdfgen_hip_last_profile(sdfgen_hip_profile *out);
 
-/* Free cached device workspaces (they are grow-only between calls).  With no slab session alive it
- * also closes the HIP IPC mappings of neighbour slabs' communication blocks; the process's own pool of
- * uncached communication blocks is kept (power-of-two size classes from 2 MiB, reused by later
- * sessions). */
+/* Free cached device workspaces (they are grow-only between calls).  The process's own pool of
+ * uncached communication blocks (power-of-two size classes from 2 MiB, reused by later sessions) and
+ * the HIP IPC mappings of neighbour slabs' blocks are kept: a freed uncached range handed to a later
+ * hipMalloc has been seen to lose stores, and an imported mapping is uncached too. */
 int sdfgen_hip_release(void);
 
 /* ---------------------------------------------------------------------------
@@ -198,6 +199,12 @@ int sdfgen_hip_slab_connect_local(sdfgen_hip_slab *s, sdfgen_hip_slab *lower, sd
  * thread that drives SEVERAL slabs must prepare all of them before it enqueues any of them: setting
  * a slab up while another slab's kernels already wait on it can block the thread. */
 int sdfgen_hip_slab_prepare(sdfgen_hip_slab *s, uint64_t ntri, char *errbuf, size_t errlen);
+/* Opt-in (ABI 5): close this process's IPC mappings of neighbour slabs' communication blocks.  Only
+ * when no slab session is alive (returns the number closed, 0 while one is).  For a long-lived process
+ * whose peer processes are replaced between jobs (a new peer's handle bytes could equal an exited
+ * one's).  The closed virtual ranges return to this process's allocator -- the situation the block
+ * pool avoids -- so the library never does this on its own. */
+int sdfgen_hip_slab_close_imports(void);
 /* Device buffers on the session's GPU; d_phi_slab receives ni*nj*(k_end-k_begin) floats in
  * the chosen layout (ARRAY3: i fastest, the slab's planes only; KFAST: k fastest). */
 int sdfgen_hip_slab_enqueue(sdfgen_hip_slab *s, const uint32_t *d_tri, uint64_t ntri, const float *d_xyz,

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 __version__ = "0.1.0"
 
+import os
 from typing import Optional, Tuple
 
 import numpy as np
@@ -57,6 +58,21 @@ def _as_nx3(a, dtype, name):
     return np.ascontiguousarray(arr, dtype=dtype)
 
 
+def _ngpu_from_env() -> int:
+    """SDFGEN_NGPU, the drop-in's GPU-count knob (the reference's signature has no device argument):
+    unset or "1" = the current device, "all" or "0" = every visible device, n > 1 = devices 0..n-1 with
+    the grid split into Z-slabs (DESIGN.md §7) -- the same rule as sdfgen::make_level_set3
+    (csrc/sdfgen_unified.cpp ngpu_from_env)."""
+    e = os.environ.get("SDFGEN_NGPU", "")
+    if e == "":
+        return _lib.NGPU_CURRENT
+    if e == "all":
+        return _lib.NGPU_ALL
+    if not e.isdigit():
+        raise ValueError(f"SDFGEN_NGPU = {e!r} (expected 'all', 0, 1 or a device count)")
+    return int(e)
+
+
 def generate_sdf(vertices, triangles, origin, dx, nx, ny, nz, exact_band=1, backend="auto", num_threads=0):
     """Generate a signed distance field (python/sdfgen_py.cpp:160-218).
 
@@ -82,7 +98,8 @@ def generate_sdf(vertices, triangles, origin, dx, nx, ny, nz, exact_band=1, back
         if not is_gpu_available():
             raise RuntimeError("GPU backend requested but no HIP GPU device is available. "
                                "Use backend='cpu'.")
-        return _lib.make_level_set3(v, t, o, float(dxf), nx, ny, nz, int(exact_band), _lib.LAYOUT_KFAST)
+        return _lib.make_level_set3(v, t, o, float(dxf), nx, ny, nz, int(exact_band), _lib.LAYOUT_KFAST,
+                                    ngpu=_ngpu_from_env())
     return _lib.cpu_make_level_set3(v, t, o, float(dxf), nx, ny, nz, int(exact_band), int(num_threads),
                                     _lib.LAYOUT_KFAST)
 

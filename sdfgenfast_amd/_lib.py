@@ -48,6 +48,7 @@ EXPORTED = (
     "sdfgen_hip_slab_run",
     "sdfgen_hip_slab_destroy",
     "sdfgen_hip_slab_prepare",
+    "sdfgen_hip_slab_close_imports",
     "sdfgen_hip_slab_debug_dump",
     "sdfgen_cpu_slab_create",
     "sdfgen_cpu_slab_range",
@@ -128,6 +129,8 @@ def _load():
     L.sdfgen_hip_last_profile.argtypes = [ctypes.POINTER(Profile)]
     L.sdfgen_hip_last_profile.restype = ctypes.c_int
     L.sdfgen_hip_release.restype = ctypes.c_int
+    if hasattr(L, "sdfgen_hip_slab_close_imports"):   # (absent from pre-ABI-5 libraries loaded for A/B runs)
+        L.sdfgen_hip_slab_close_imports.restype = ctypes.c_int
     L.sdfgen_cpu_make_level_set3.argtypes = [_P, _u64, _P, _u64, _P, ctypes.c_float, ctypes.c_int, ctypes.c_int,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _P,
                                              ctypes.c_char_p, ctypes.c_size_t]
@@ -316,7 +319,14 @@ def last_profile() -> dict:
 
 
 def release() -> None:
+    """Free the cached device workspaces (the slab communication pool and IPC mappings stay)."""
     lib.sdfgen_hip_release()
+
+
+def slab_close_imports() -> int:
+    """Opt-in: close the IPC mappings of neighbour slabs' blocks once no slab session is alive
+    (sdfgen_hip_slab_close_imports; for long-lived processes whose peers are replaced between jobs)."""
+    return int(lib.sdfgen_hip_slab_close_imports())
 
 
 def debug_ptd(pts: np.ndarray, device: int = 0, variant: int = 0) -> np.ndarray:

@@ -41,6 +41,17 @@ inline hipError_t zero_async(void *p, size_t bytes, hipStream_t st)
     hipLaunchKernelGGL(k_zero32<>, dim3(blocks), dim3(256), 0, st, (uint32_t *)p, n);
     return hipGetLastError();
 }
+// The HIP status behind the last failed runtime call of this thread's sweep set-up helpers
+// (st_grow, sp_grow, the stream syncs before a buffer grows): their error messages name it, so a
+// sticky fault of an earlier kernel surfaces as that fault, not as "allocation failed".
+inline thread_local hipError_t sdf_last_hip = hipSuccess;
+// Record e and map it to the library's status: -5 (out of memory) or -4 (runtime / kernel error).
+inline int sdf_hip_rc(hipError_t e)
+{
+    sdf_last_hip = e;
+    return (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) ? -5 : -4;
+}
+inline const char *sdf_last_hip_name() { return sdf_last_hip == hipSuccess ? "no HIP error recorded" : hipGetErrorName(sdf_last_hip); }
 #endif
 
 // IEEE correctly-rounded float sqrt and division on both sides.  NOTE: on ROCm 7.2

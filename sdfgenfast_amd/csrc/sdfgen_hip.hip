@@ -4,7 +4,7 @@
 // Pipeline (one HIP stream per call):
 //   k_prep   : gather the indexed mesh into a per-triangle vertex soup (48 B/tri),
 //              validate indices, initialise the cell state         (:196-199)
-//   k_band_lds: batches of 32 consecutive triangles per workgroup -- exact distances over
+//   k_band_lds: batches of BAND_BT (64) consecutive triangles per workgroup -- exact distances over
 //              the band boxes, merged per cell in LDS, then one global atomicMin on the
 //              packed u64 key (f32bits(d)<<32 | t) that reproduces the CPU's
 //              ascending-t strict-< rule; ray-parity counts (:203-236)
@@ -100,9 +100,11 @@ __global__ void k_prep_soup(const uint32_t *__restrict__ tri, uint64_t ntri, con
                 atomicOr(err_flag, 1);
                 q = 0;
             }
-            x[c] = mk3(xyz[3 * q + 0], xyz[3 * q + 1], xyz[3 * q + 2]);
+            const uint64_t xq = SDF_CHK(40, 3 * q, 0, 3 * nvert);
+            x[c] = mk3(xyz[xq + 0], xyz[xq + 1], xyz[xq + 2]);
         }
         // w of the third vertex: the triangle's tri_invdet (read by every ptd_wave / ptd_wave2)
+        (void)SDF_CHK(41, 3 * t + 2, 0, 3 * ntri);
         soup[3 * t + 0] = make_float4(x[0].x, x[0].y, x[0].z, 0.0f);
         soup[3 * t + 1] = make_float4(x[1].x, x[1].y, x[1].z, 0.0f);
         soup[3 * t + 2] = make_float4(x[2].x, x[2].y, x[2].z, tri_invdet(x[0], x[1], x[2]));
@@ -228,14 +230,18 @@ __device__ __forceinline__ void lat_box(const double f[9], const Grid &g, int k_
 }
 
 // One lattice point of the ray-parity test (:226-235).
-__device__ __forceinline__ void parity_point(const double *f, int j, int k, const Grid &g, uint32_t *cnt)
+__device__ __forceinline__ void parity_point(const double *f, int j, int k, const Grid &g, uint32_t *cnt, int k_lo, int k_hi)
 {
+    (void)k_lo;
+    (void)k_hi;
     double a, b, cc;
     if (pit2d((double)j, (double)k, f[1], f[2], f[4], f[5], f[7], f[8], a, b, cc)) {
         const double fi = (a * f[0] + b * f[3]) + cc * f[6];
         const int ii = trunc_to_int(ceil(fi));
-        if (ii < 0) atomicAdd(cnt + cidx(0, j, k, g.ni, g.nj), 1u);
-        else if (ii < g.ni) atomicAdd(cnt + cidx(ii, j, k, g.ni, g.nj), 1u);
+        // (bounds builds: k of a lattice point lies in the slab's planes; the range is the slab's cnt)
+        [[maybe_unused]] const size_t plane = (size_t)g.ni * g.nj;
+        if (ii < 0) atomicAdd(cnt + SDF_CHK(45, cidx(0, j, k, g.ni, g.nj), plane * k_lo, plane * k_hi), 1u);
+        else if (ii < g.ni) atomicAdd(cnt + SDF_CHK(45, cidx(ii, j, k, g.ni, g.nj), plane * k_lo, plane * k_hi), 1u);
     }
 }
 
@@ -373,14 +379,17 @@ __global__ void __launch_bounds__(256, BAND_WPE) k_band_lds(const float4 *__rest
             for (unsigned c = tid; c < uvol; c += 256) s_key[c] = ~0ull;
         // the batch's ray-lattice points over all 256 threads (:222-235)
         for (unsigned fl = tid; fl < ltotal; fl += 256) {
-            const int q = find_q(s_lpre, nb, fl);
+            const int q = (int)SDF_CHK(42, find_q(s_lpre, nb, fl), 0, nb);
             const LatBox L = s_lat[q];
             const unsigned r = fl - s_lpre[q], kk = r / (unsigned)L.nj;
-            parity_point(s_f[q], L.j0 + (int)(r - kk * (unsigned)L.nj), L.k0 + (int)kk, g, cnt);
+            parity_point(s_f[q], L.j0 + (int)(r - kk * (unsigned)L.nj), L.k0 + (int)kk, g, cnt, k_lo, k_hi);
         }
         __syncthreads();
         // (triangle, cell) pair of flat index fl (triangle q of the batch)
         auto pair_in = [&](int q, unsigned fl, int &i, int &j, int &k) {
+            // bounds builds: the pair's triangle is one of the batch's, and fl lies in its box
+            q = (int)SDF_CHK(42, q, 0, nb);
+            (void)SDF_CHK(43, fl, s_pre[q], s_pre[q + 1]);
             const BandBox B = s_box[q];
             const unsigned r = fl - s_pre[q], bij = (unsigned)(B.bi * B.bj);
 #if BAND_FDIV
@@ -408,9 +417,10 @@ __global__ void __launch_bounds__(256, BAND_WPE) k_band_lds(const float4 *__rest
             if (d < init) {   // also rejects NaN
                 const u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
                 if (merge) {
-                    atomicMin(&s_key[(unsigned)((k - uk0) * unj + (j - uj0)) * (unsigned)uni + (unsigned)(i - ui0)], key);
+                    atomicMin(&s_key[SDF_CHK(46, (unsigned)((k - uk0) * unj + (j - uj0)) * (unsigned)uni + (unsigned)(i - ui0), 0,
+                                             uvol)], key);
                 } else {
-                    u64 *p = cell + cidx(i, j, k, g.ni, g.nj);
+                    u64 *p = cell + SDF_CHK(44, cidx(i, j, k, g.ni, g.nj), (size_t)g.ni * g.nj * k_lo, (size_t)g.ni * g.nj * k_hi);
                     if (key < *p) atomicMin(p, key);
                 }
             }
@@ -440,7 +450,7 @@ __global__ void __launch_bounds__(256, BAND_WPE) k_band_lds(const float4 *__rest
                 pair_in(qb, two ? fb : fa, i2, j2, k2);
                 const f3 gx = mk3((float)i * g.dx + g.ox, (float)j * g.dx + g.oy, (float)k * g.dx + g.oz);
                 const f3 gx2 = mk3((float)i2 * g.dx + g.ox, (float)j2 * g.dx + g.oy, (float)k2 * g.dx + g.oz);
-                const float4 *sa = soup + 3 * (t0 + qa), *sb = soup + 3 * (t0 + qb);
+                const float4 *sa = soup + 3 * SDF_CHK(47, t0 + qa, 0, ntri), *sb = soup + 3 * SDF_CHK(47, t0 + qb, 0, ntri);
                 const float4 a0 = sa[0], a1 = sa[1], a2 = sa[2], b0 = sb[0], b1 = sb[1], b2 = sb[2];
                 float d, d2 = 0.0f;
 #if BAND_DIAG_NOPTD
@@ -467,7 +477,8 @@ __global__ void __launch_bounds__(256, BAND_WPE) k_band_lds(const float4 *__rest
                 const u64 key = s_key[c];
                 if (key == ~0ull) continue;
                 const unsigned ij = (unsigned)(uni * unj), kk = c / ij, rem = c - kk * ij, jj = rem / (unsigned)uni;
-                u64 *p = cell + cidx(ui0 + (int)(rem - jj * (unsigned)uni), uj0 + (int)jj, uk0 + (int)kk, g.ni, g.nj);
+                u64 *p = cell + SDF_CHK(44, cidx(ui0 + (int)(rem - jj * (unsigned)uni), uj0 + (int)jj, uk0 + (int)kk, g.ni, g.nj),
+                                        (size_t)g.ni * g.nj * k_lo, (size_t)g.ni * g.nj * k_hi);
                 atomicMin(p, key);   // no load-compare first: 0.81 -> 0.78 ms at C3 (no return to wait for)
             }
         __syncthreads();
@@ -532,7 +543,7 @@ __global__ void __launch_bounds__(256) k_band_big(const float4 *__restrict__ sou
             lo += (c - 1) * step;
             hi = min(hi, lo + step);
         }
-        const uint32_t e = lo;
+        const uint32_t e = (uint32_t)SDF_CHK(48, lo, 0, n);
         const uint64_t t = big.tri[e];
         BandBox B;
         LatBox L;
@@ -564,7 +575,7 @@ __global__ void __launch_bounds__(256) k_band_big(const float4 *__restrict__ sou
             auto emit = [&](float d, int i, int j, int k) {
                 if (d < init) {   // also rejects NaN
                     const u64 key = ((u64)__float_as_uint(d) << 32) | (u64)(uint32_t)t;
-                    u64 *p = cell + cidx(i, j, k, g.ni, g.nj);
+                    u64 *p = cell + SDF_CHK(44, cidx(i, j, k, g.ni, g.nj), (size_t)g.ni * g.nj * k_lo, (size_t)g.ni * g.nj * k_hi);
                     if (key < *p) atomicMin(p, key);
                 }
             };
@@ -587,7 +598,7 @@ __global__ void __launch_bounds__(256) k_band_big(const float4 *__restrict__ sou
             const uint32_t nvalid = (uint32_t)min<uint64_t>(BAND_CH_LAT, lat - b0);
             for (uint32_t r = lane; r < nvalid; r += 64) {
                 const uint32_t jj = rj + r, ck = jj / (uint32_t)L.nj;
-                parity_point(f, L.j0 + (int)(jj - ck * (uint32_t)L.nj), L.k0 + (int)(rk + ck), g, cnt);
+                parity_point(f, L.j0 + (int)(jj - ck * (uint32_t)L.nj), L.k0 + (int)(rk + ck), g, cnt, k_lo, k_hi);
             }
         }
     }
@@ -697,7 +708,8 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
     const uint64_t rstep = ((uint64_t)gridDim.x * blockDim.x) >> 6;   // grid-stride over rows (capped grid)
     for (uint64_t row = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6; row < nrows; row += rstep) {
         const int j = (int)(row % g.nj), k = k_lo + (int)(row / g.nj);
-        const size_t base = cidx(0, j, k, g.ni, g.nj);
+        const size_t base = SDF_CHK(49, cidx(0, j, k, g.ni, g.nj), (size_t)g.ni * g.nj * k_lo,
+                                    (size_t)g.ni * g.nj * (k_lo + k_cnt));
         uint32_t carry = 0;
         for (int i0 = 0; i0 < g.ni; i0 += 64) {
             const int i = i0 + lane;
@@ -710,8 +722,10 @@ __global__ void __launch_bounds__(256) k_sign(const u64 *__restrict__ cell, cons
                 uint32_t bits = (uint32_t)(cell[base + i] >> 32);
                 if (pre) bits ^= 0x80000000u;
                 float v = __uint_as_float(bits);
-                if (layout == SDFGEN_LAYOUT_ARRAY3) out[cidx(i, j, k - k_lo, g.ni, g.nj)] = v;
-                else out[((size_t)i * g.nj + j) * k_cnt + (k - k_lo)] = v;
+                const size_t nout = (size_t)g.ni * g.nj * k_cnt;
+                if (layout == SDFGEN_LAYOUT_ARRAY3) out[SDF_CHK(50, cidx(i, j, k - k_lo, g.ni, g.nj), 0, nout)] = v;
+                else out[SDF_CHK(50, ((size_t)i * g.nj + j) * k_cnt + (k - k_lo), 0, nout)] = v;
+                (void)nout;
             }
             carry = (carry + (uint32_t)__popcll(mask)) & 1u;
         }
@@ -744,7 +758,8 @@ __global__ void __launch_bounds__(256) k_sign_kfast(const u64 *__restrict__ cell
             for (int r = 0; r < 16; ++r) {   // rows kb + 16 w + r (wave-uniform)
                 const int kr = kb + 16 * w + r;
                 if (kr < k_cnt) {
-                    const size_t base = cidx(0, j, k_lo + kr, g.ni, g.nj);
+                    const size_t base = SDF_CHK(49, cidx(0, j, k_lo + kr, g.ni, g.nj), (size_t)g.ni * g.nj * k_lo,
+                                                (size_t)g.ni * g.nj * (k_lo + k_cnt));
                     const uint32_t par = ok ? (cnt[base + i] & 1u) : 0u;
                     const u64 mask = __ballot(par);
                     const uint32_t pre = (carry[r] + (uint32_t)__popcll(mask & below)) & 1u;
@@ -757,7 +772,7 @@ __global__ void __launch_bounds__(256) k_sign_kfast(const u64 *__restrict__ cell
             __syncthreads();
             const int kk = kb + lane;
             for (int ii = w; ii < 64 && i0 + ii < g.ni; ii += 4)
-                if (kk < k_cnt) out[((size_t)(i0 + ii) * g.nj + j) * k_cnt + kk] = s_t[lane][ii];
+                if (kk < k_cnt) out[SDF_CHK(50, ((size_t)(i0 + ii) * g.nj + j) * k_cnt + kk, 0, (size_t)g.ni * g.nj * k_cnt)] = s_t[lane][ii];
             __syncthreads();
         }
     }
@@ -1065,8 +1080,9 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
         if (!do_sweep || s >= nsweeps) continue;
         const int di = SWEEP_DIRS[s % 8][0], dj = SWEEP_DIRS[s % 8][1], dk = SWEEP_DIRS[s % 8][2];
         if (impl == 1 && s >= sparse_first) {
+            sdf_last_hip = hipSuccess;
             if ((rc = sparse_sweep(ws->sp, st, ws->soup, &ws->cell, &ws->cap_cell, origin, dx, ni, nj, nk, s)))
-                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU sparse sweep setup failed");
+                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU sparse sweep setup failed: %s", sdf_last_hip_name());
             launches += 2;
             ++sparse_sweeps;
             continue;
@@ -1382,8 +1398,8 @@ int comm_export(char *p, hipIpcMemHandle_t *h, Err &err)
 // long-lived peer processes add none after their first sessions).  Keyed by the handle bytes: a handle
 // is only ever reused by the exporting process for the same block (hipIpcGetMemHandle of a live
 // allocation), and a peer that exited and a new one whose handle bytes collide would map a stale block --
-// callers that replace peer processes call sdfgen_hip_release in the survivors between jobs: with no slab
-// session alive it closes every imported mapping (comm_close_imports).
+// callers that replace peer processes call sdfgen_hip_slab_close_imports in the survivors between jobs
+// (opt-in: with no slab session alive it closes every imported mapping, comm_close_imports).
 struct CommImport {
     int device;
     hipIpcMemHandle_t handle;
@@ -1391,6 +1407,30 @@ struct CommImport {
 };
 std::vector<CommImport> g_comm_imports;
 int g_live_slabs = 0;   // slab sessions alive in this process (under g_comm_mu)
+std::vector<int> g_dev_slabs;   // ... per device (under g_comm_mu)
+
+// Slab sessions sharing `device`: this process's live ones, or SDFGEN_SLABS_PER_DEVICE when the caller
+// knows of more (ranks of other processes on the same GPU -- a one-GPU rehearsal of a multi-GPU run).
+int slab_share(int device)
+{
+    int n = 1;
+    {
+        std::lock_guard<std::mutex> lk(g_comm_mu);
+        if (device >= 0 && (size_t)device < g_dev_slabs.size()) n = std::max(n, g_dev_slabs[device]);
+    }
+    if (const char *e = getenv("SDFGEN_SLABS_PER_DEVICE")) n = std::max(n, atoi(e));
+    return n;
+}
+
+// Hardware queues the HIP runtime gives this process per device (its GPU_MAX_HW_QUEUES, default 4).
+// Slab sessions of one device whose streams share a hardware queue run their kernels one after the
+// other -- and a slab's kernels wait on its neighbours' -- so more sessions than queues cannot work.
+int hw_queues()
+{
+    const char *e = getenv("GPU_MAX_HW_QUEUES");
+    const int q = e ? atoi(e) : 4;
+    return q > 0 ? q : 4;
+}
 
 // Close every imported neighbour mapping once no slab session of this process is alive.  Returns the
 // number closed (0 while a session is alive).
@@ -1480,6 +1520,8 @@ int slab_alloc(SlabSession *S, Err &err)
     {
         std::lock_guard<std::mutex> lk(g_comm_mu);
         ++g_live_slabs;
+        if ((size_t)S->device >= g_dev_slabs.size()) g_dev_slabs.resize(S->device + 1, 0);
+        ++g_dev_slabs[S->device];
     }
     HIPCHK(hipMemset(S->comm, 0, S->cl.bytes));   // epoch 0 is never published, flags start at 0
     HIPCHK(hipDeviceSynchronize());
@@ -1496,6 +1538,7 @@ void slab_free(SlabSession *S)
         comm_return(S->comm);
         std::lock_guard<std::mutex> lk(g_comm_mu);
         --g_live_slabs;
+        if ((size_t)S->device < g_dev_slabs.size()) --g_dev_slabs[S->device];
     }
     S->comm = nullptr;
     (void)hipFree(S->cell_mem);
@@ -1587,7 +1630,7 @@ int slab_prepare(SlabSession *S, uint64_t ntri, Err &err)
         slab_c_range(S, dk, &cs, &ce);
         if (ni >= 2 && nj >= 2 && ce > cs)
             if (int rc = st_prepare(S->wf, st, ni, nj, cs, ce, &ti))
-                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab buffers");
+                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab buffers: %s", sdf_last_hip_name());
     }
     if (ni >= 2 && nj >= 2 && nk >= 2 && slab_multi_on()) {
         StSlabPlan plan;
@@ -1600,7 +1643,7 @@ int slab_prepare(SlabSession *S, uint64_t ntri, Err &err)
     }
     if (slab_sparse_on(S)) {
         if (int rc = sp_reserve(S->sp, plane_cells * kc, st))
-            return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse buffers");
+            return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse buffers: %s", sdf_last_hip_name());
         if (!S->alt_mem) {
             HIPCHK(hipMalloc((void **)&S->alt_mem, plane_cells * kc * sizeof(u64)));
             S->alt = S->alt_mem - plane_cells * (size_t)S->k_begin;
@@ -1664,8 +1707,13 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
     S->sparse_sweeps = 0;
     S->tile_multi = 0;
     {
-        const char *gr = getenv("SDFGEN_TILE_GRID");   // co-resident slabs on one GPU need a cap
+        // Co-resident slabs on one GPU: each slab's persistent grids are capped by the library (sweep_tile.hpp
+        // st_share_grid, sp_share_workers) from the occupancy query and the slab sessions sharing the device,
+        // so that every slab keeps workgroups resident while its neighbours wait on it; SDFGEN_TILE_GRID
+        // overrides (diagnostics)
+        const char *gr = getenv("SDFGEN_TILE_GRID");
         S->wf.grid_override = gr ? atoi(gr) : 0;
+        S->wf.share = slab_share(S->device);
     }
     S->wf.clo = plane_cells * (uint64_t)S->k_begin;
     S->wf.chi = plane_cells * (uint64_t)S->k_end;
@@ -1700,8 +1748,12 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
         // second pass as Jacobi + repair per slab, in place (alt keeps the changed cells' pre-sweep
         // values) unless SDFGEN_SPARSE_INPLACE=0: then the state alternates between cell and alt
         {
-            const char *e = getenv("SDFGEN_SPARSE_WORKERS");
+            const char *e = getenv("SDFGEN_SPARSE_WORKERS");   // diagnostics
             S->sp.workers = e ? atoi(e) : sp_workers_for((unsigned long long)ni * nj * (S->k_end - S->k_begin));
+            // a slab's repair kernel ends only after its upstream neighbour's: with several slabs on one GPU
+            // every one of them must stay resident (8 x 256 one-wave workgroups at 171 VGPRs are the chip's
+            // 2,048 slots for them -- the repair watchdogs fired without a cap)
+            if (!e) S->sp.workers = std::min(S->sp.workers, sp_share_workers(slab_share(S->device)));
             const char *ip = getenv("SDFGEN_SPARSE_INPLACE");
             S->sp.inplace = !(ip && atoi(ip) == 0);
         }
@@ -1756,7 +1808,7 @@ int slab_enqueue(SlabSession *S, const uint32_t *d_tri, uint64_t ntri, const flo
             L.tm = S->tm;
             L.tm_m = m;
             if (int rc = sparse_sweep_slab(S->sp, st, S->soup, L, origin, dx, ni, nj, nk, s))
-                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse sweep setup failed");
+                return err.set(rc == -5 ? SDFGEN_HIP_ENOMEM : SDFGEN_HIP_ERUNTIME, "GPU slab sparse sweep setup failed: %s", sdf_last_hip_name());
             S->launches += 3;
             ++S->sparse_sweeps;
             if (!S->sp.inplace) std::swap(cur, other);
@@ -2120,6 +2172,7 @@ int sdfgen_hip_debug_band(const uint32_t *tri, uint64_t ntri, const float *xyz, 
     std::vector<u64> cells(n);
     HIPCHK(hipMemcpyAsync(cells.data(), ws->cell, n * sizeof(u64), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if ((rc = check_oob(err, "debug_band"))) return rc;
     if (flag) return err.set(SDFGEN_HIP_EINDEX, "triangle vertex index out of range (>= %llu vertices)",
                              (unsigned long long)nvert);
     for (uint64_t q = 0; q < n; ++q) {
@@ -2162,10 +2215,16 @@ int sdfgen_hip_release(void)
         delete w;
     }
     g_ws.clear();
-    // imported neighbour blocks (Z-slabs over IPC): closed once no slab session is alive; the pool of
-    // uncached communication blocks is kept (freeing them is what the pool avoids)
-    comm_close_imports();
+    // the pool of uncached communication blocks and the imported neighbour blocks (Z-slabs over IPC) are
+    // kept: freeing them is what the pool avoids; sdfgen_hip_slab_close_imports is the
+    // caller's explicit choice
     return 0;
+}
+
+int sdfgen_hip_slab_close_imports(void)
+{
+    DeviceGuard dg_;
+    return comm_close_imports();
 }
 
 int sdfgen_hip_debug_sweep_trace(int device, uint64_t *out, uint64_t max_entries, uint64_t *n_out)
@@ -2241,6 +2300,18 @@ int sdfgen_hip_slab_create(int device, int nslabs, int slab, int ni, int nj, int
     if (nslabs < 1 || slab < 0 || slab >= nslabs) return err.set(SDFGEN_HIP_EINVAL, "slab %d of %d", slab, nslabs);
     if (nk < 2 * nslabs) return err.set(SDFGEN_HIP_EINVAL, "nz = %d too small for %d slabs (need >= 2 planes each)", nk, nslabs);
     if (device < 0 || device >= device_count_impl()) return err.set(SDFGEN_HIP_ENODEV, "GPU device %d not available", device);
+    {
+        int live = 0;
+        {
+            std::lock_guard<std::mutex> lk(g_comm_mu);
+            if ((size_t)device < g_dev_slabs.size()) live = g_dev_slabs[device];
+        }
+        if (live + 1 > hw_queues())
+            return err.set(SDFGEN_HIP_EINVAL,
+                           "%d slab sessions on device %d need as many hardware queues; this process has %d "
+                           "(GPU_MAX_HW_QUEUES): slabs sharing a queue would run one after the other while each waits "
+                           "on its neighbours", live + 1, device, hw_queues());
+    }
     sdfgen_hip_slab *h = new sdfgen_hip_slab();
     SlabSession *S = &h->s;
     S->device = device;

@@ -9,6 +9,8 @@
 // reference caller's object files import.
 #include "sdfgen/sdfgen_unified.h"
 
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -38,6 +40,23 @@ void prepare(int nx, int ny, int nz, Array3f &phi)
     phi.resize(nx, ny, nz);
 }
 
+// The GPU-count knob of the drop-in (Config row): the reference's signatures have no
+// device argument (common/sdfgen_unified.h:47-57), so SDFGEN_NGPU picks the devices -- unset or "1": the
+// current device (the reference's behaviour, gpu_lib/makelevelset3_gpu.cu:600-603); "all" or "0": every
+// visible device; n > 1: devices 0..n-1, the grid split into Z-slabs.  Anything else
+// is a std::invalid_argument.
+int ngpu_from_env()
+{
+    const char *e = std::getenv("SDFGEN_NGPU");
+    if (!e || !*e) return SDFGEN_NGPU_CURRENT;
+    if (std::strcmp(e, "all") == 0) return SDFGEN_NGPU_ALL;
+    char *end = nullptr;
+    const long n = std::strtol(e, &end, 10);
+    if (end == e || *end != 0 || n < 0 || n > 4096)
+        throw std::invalid_argument(std::string("SDFGEN_NGPU = '") + e + "' (expected 'all', 0, 1 or a device count)");
+    return (int)n;
+}
+
 const uint32_t *tri_ptr(const std::vector<Vec3ui> &tri)
 {
     return tri.empty() ? nullptr : reinterpret_cast<const uint32_t *>(tri.data());  // packed uint32[n][3]
@@ -59,7 +78,7 @@ void make_level_set3(const std::vector<Vec3ui> &tri, const std::vector<Vec3f> &x
     char err[512] = {0};
     const float o[3] = {origin[0], origin[1], origin[2]};
     const int rc = sdfgen_hip_make_level_set3(tri_ptr(tri), tri.size(), xyz_ptr(x), x.size(), o, dx, nx, ny, nz,
-                                              exact_band, SDFGEN_NGPU_CURRENT, SDFGEN_LAYOUT_ARRAY3, phi.a.data, err,
+                                              exact_band, ngpu_from_env(), SDFGEN_LAYOUT_ARRAY3, phi.a.data, err,
                                               sizeof(err));
     if (rc != 0) throw_for(rc, err);
 }

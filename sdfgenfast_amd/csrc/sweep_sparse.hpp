@@ -1615,11 +1615,21 @@ template <class T>
 inline int sp_grow(T **p, size_t *cap, size_t need, bool zero, hipStream_t st)
 {
     if (*p && *cap >= need) return 0;
-    if (*p) (void)hipFree(*p);
+    if (*p) {
+        const hipError_t e = hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        if (e != hipSuccess) return sdf_hip_rc(e);   // (a sticky fault of an earlier kernel: see st_grow)
+    }
     *p = nullptr;
     *cap = 0;
-    if (hipMalloc((void **)p, need * sizeof(T)) != hipSuccess) return -5;
-    if (zero && hipMemsetAsync(*p, 0, need * sizeof(T), st) != hipSuccess) return -4;   // (see st_grow)
+    if (hipError_t e = hipMalloc((void **)p, need * sizeof(T)); e != hipSuccess) {
+        *p = nullptr;
+        return sdf_hip_rc(e);
+    }
+    if (zero) {
+        if (hipError_t e = hipMemsetAsync(*p, 0, need * sizeof(T), st); e != hipSuccess) return sdf_hip_rc(e);
+    }
     *cap = need;
     return 0;
 }
@@ -1641,16 +1651,16 @@ inline unsigned long long sp_jblocks(unsigned long long n)
 inline int sp_reserve(SparseSweepWorkspace &W, unsigned long long n, hipStream_t st)
 {
     const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
-    if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;
-    if (sp_grow(&W.queue, &W.cap_queue, sp_shards(n) * cap, true, st)) return -5;
+    if (int rc_ = sp_grow(&W.req, &W.cap_req, n, true, st)) return rc_;
+    if (int rc_ = sp_grow(&W.queue, &W.cap_queue, sp_shards(n) * cap, true, st)) return rc_;
     if (!W.ctl) {
-        if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
-        if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
+        if (hipError_t e = hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)); e != hipSuccess) return sdf_hip_rc(e);
+        if (hipError_t e = hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st); e != hipSuccess) return sdf_hip_rc(e);
     }
     const unsigned long long blocks = sp_jblocks(n);
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
     const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
-    if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
+    if (int rc_ = sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return rc_;
     return 0;
 }
 
@@ -1662,22 +1672,22 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
 {
     const int di = SP_DIRS[sweep % 8][0], dj = SP_DIRS[sweep % 8][1], dk = SP_DIRS[sweep % 8][2];
     const unsigned long long cap = n + SP_WORKERS * 64ull + 1024ull;
-    if (sp_grow(&W.req, &W.cap_req, n, true, st)) return -5;      // stays all-zero between sweeps
-    if (sp_grow(&W.queue, &W.cap_queue, sp_shards(n) * cap, true, st)) return -5; // slots are reset when consumed
+    if (int rc_ = sp_grow(&W.req, &W.cap_req, n, true, st)) return rc_;      // stays all-zero between sweeps
+    if (int rc_ = sp_grow(&W.queue, &W.cap_queue, sp_shards(n) * cap, true, st)) return rc_; // slots are reset when consumed
     if (!W.ctl) {
-        if (hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)) != hipSuccess) return -5;
-        if (hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st) != hipSuccess) return -4;
+        if (hipError_t e = hipMalloc((void **)&W.ctl, SP_NCTL * sizeof(unsigned long long)); e != hipSuccess) return sdf_hip_rc(e);
+        if (hipError_t e = hipMemsetAsync(W.ctl, 0, SP_NCTL * sizeof(unsigned long long), st); e != hipSuccess) return sdf_hip_rc(e);
     }
     // per sweep: reset the list counters; error bits and statistics accumulate over the call
-    if (zero_async(W.ctl + SP_QUEUE, (SP_DIAGX - SP_QUEUE) * sizeof(unsigned long long), st) != hipSuccess)
-        return -4;
+    if (hipError_t e = zero_async(W.ctl + SP_QUEUE, (SP_DIAGX - SP_QUEUE) * sizeof(unsigned long long), st); e != hipSuccess)
+        return sdf_hip_rc(e);
     blocks = sp_jblocks(n);
     // each list part holds every cell its blocks visit (~n/64), so it never overflows; sizing
     // it for the ~10 % that are listed would need an in-place fallback whose registers
     // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
     const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
-    if (sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return -5;
+    if (int rc_ = sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return rc_;
     memset(&P, 0, sizeof(P));
     P.soup = soup;
     P.req = W.req - c_lo;
@@ -1735,7 +1745,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
 {
     const unsigned long long n = (unsigned long long)ni * nj * nk;
     const int nw = (W.workers > 0 && W.workers <= SP_WORKERS) ? W.workers : SP_WORKERS;
-    if (sp_grow(&W.alt, &W.cap_alt, n, false, st)) return -5;
+    if (int rc_ = sp_grow(&W.alt, &W.cap_alt, n, false, st)) return rc_;
     SpParams P;
     unsigned long long blocks = 0;
     if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, 0, n, P, blocks)) return rc;
@@ -1747,38 +1757,38 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         B.nbj = (nj + SPB - 1) / SPB;
         B.nbk = (nk + SPB - 1) / SPB;
         B.nbricks = (unsigned long long)B.nbi * B.nbj * B.nbk;
-        if (sp_grow(&W.breq, &W.cap_breq, B.nbricks, true, st)) return -5;
-        if (sp_grow(&W.bbits, &W.cap_bbits, B.nbricks * SPB_WORDS, true, st)) return -5;
+        if (int rc_ = sp_grow(&W.breq, &W.cap_breq, B.nbricks, true, st)) return rc_;
+        if (int rc_ = sp_grow(&W.bbits, &W.cap_bbits, B.nbricks * SPB_WORDS, true, st)) return rc_;
         B.breq = W.breq;
         B.bits = W.bbits;
         sp_launch_jacobi(blocks, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_jlist_brick, dim3(32 * SP_JPARTS), dim3(256), 0, st, P, B);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_brick, dim3(nw), dim3(64), 0, st, P, B);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
     } else if (W.inplace) {
         // in place: the cells that keep their value (~99.9 %) are neither copied nor swapped
         P.S = *cell;
         P.X = *cell;
         P.sv = W.alt;
         sp_launch_jacobi(blocks, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_jlist<false>, dim3(SP_JLIST_PER_PART * SP_JPARTS), dim3(256), 0, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         return 0;
     } else {
         P.S = *cell;
         P.X = W.alt;
         sp_launch_jacobi(blocks, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         const unsigned long long lblocks = SP_JLIST_PER_PART * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
         hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
-        if (hipGetLastError() != hipSuccess) return -4;
+        if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
     }
     // swap the state buffers (both hold n cells)
     unsigned long long *t = *cell;
@@ -1836,7 +1846,7 @@ inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const floa
     H.word = SP_FL_DONE;
     H.epoch = L.prev_epoch;
     hipLaunchKernelGGL(k_sp_slab_wait, dim3(1), dim3(64), 0, st, H);
-    if (hipMemsetAsync(L.arrive, 0, sizeof(unsigned), st) != hipSuccess) return -4;
+    if (hipError_t e_ = hipMemsetAsync(L.arrive, 0, sizeof(unsigned), st); e_ != hipSuccess) return sdf_hip_rc(e_);
     H.epoch = L.epoch;
     hipLaunchKernelGGL(k_sp_slab_halo, dim3((unsigned)std::min<unsigned long long>((plane + 255) / 256, 256)),
                        dim3(256), 0, st, H);
@@ -1870,8 +1880,25 @@ inline int sparse_sweep_slab(SparseSweepWorkspace &W, hipStream_t st, const floa
     const unsigned long long lblocks = 32 * SP_JPARTS;
     if (stage >= 3) hipLaunchKernelGGL(k_sp_jlist<true>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
     if (stage >= 4) hipLaunchKernelGGL(k_sp_recheck<true>, dim3(nw), dim3(64), 0, st, P);
-    if (hipGetLastError() != hipSuccess) return -4;
+    if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
     return 0;
+}
+
+// Repair workgroups of one slab when `share` slab sessions run on the current device: a quarter of the
+// chip's resident k_sp_recheck<true> workgroups split between them (share 8 at 171 VGPRs: 64 each;
+// share 1 and 2 keep the default), so the slabs' repair kernels and the first-pass grids of slabs still
+// in their first pass fit together with room for uneven placement.
+inline int sp_share_workers(int share)
+{
+    if (share <= 1) return SP_WORKERS;
+    int occ = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_sp_recheck<true>, 64, 0) != hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        occ = 8;
+        cus = 256;
+    }
+    return std::max(16, occ * cus / (4 * share));
 }
 
 inline void sparse_sweep_release(SparseSweepWorkspace &W)

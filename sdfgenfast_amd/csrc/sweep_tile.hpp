@@ -1673,6 +1673,7 @@ struct TileSweepWorkspace {
     bool trace_multi = false;  // trace every task of the one-launch first pass (diagnostics)
     int cur_sweep = 0;
     int grid_override = 0;     // diagnostics: cap on resident workgroups
+    int share = 1;             // slab sessions sharing this device (st_share_grid caps the grid when > 1)
     int lead_override = -1;    // diagnostics: smaller inter-wave lead (>= 0)
     bool skip_seen = true;     // the "already examined" skip (diagnostics can turn it off)
     unsigned long long clo = 0, chi = ~0ull, ntri = ~0ull;   // address bounds for bounds-checked builds
@@ -1710,17 +1711,42 @@ inline bool tile_sweep_supported(int ni, int nj, int nk) { return ni >= 2 && nj 
 // dies, a sync of THAT stream): a synchronous hipMemset/hipMemcpy was measured to block until
 // other streams' kernels finished -- with Z-slabs driven from one thread those kernels wait on
 // the very slab being set up.
+// Returns 0, or -5 / -4 with the failing status in sdf_last_hip (a sticky fault of an earlier kernel
+// fails the hipFree or hipMalloc here with that fault's name, not as an allocation failure).
 inline int st_grow(unsigned long long **p, size_t *cap, size_t need, hipStream_t st)
 {
     if (*p && *cap >= need) return 0;
-    if (*p) (void)hipFree(*p);
+    if (*p) {
+        const hipError_t e = hipFree(*p);
+        *p = nullptr;
+        *cap = 0;
+        if (e != hipSuccess) return sdf_hip_rc(e);
+    }
     *p = nullptr;
     *cap = 0;
-    if (hipMalloc((void **)p, need * sizeof(unsigned long long)) != hipSuccess) return -5;
+    if (hipError_t e = hipMalloc((void **)p, need * sizeof(unsigned long long)); e != hipSuccess) {
+        *p = nullptr;
+        return sdf_hip_rc(e);
+    }
     // tags are epochs >= 1: zeroed granules can never look published
-    if (hipMemsetAsync(*p, 0, need * sizeof(unsigned long long), st) != hipSuccess) return -4;
+    if (hipError_t e = hipMemsetAsync(*p, 0, need * sizeof(unsigned long long), st); e != hipSuccess) return sdf_hip_rc(e);
     *cap = need;
     return 0;
+}
+// Drain the stream before a buffer it may still read is replaced; a failed earlier kernel shows here.
+inline int st_sync(hipStream_t st)
+{
+    const hipError_t e = hipStreamSynchronize(st);
+    return e == hipSuccess ? 0 : sdf_hip_rc(e);
+}
+// "GPU tile sweep: <what>: <HIP status>" (every set-up failure names the runtime's status)
+inline int st_fail_msg(char *err, size_t errlen, int code, const char *what)
+{
+    if (err && errlen) {
+        if (code == -4 || code == -5) snprintf(err, errlen, "GPU tile sweep: %s: %s", what, sdf_last_hip_name());
+        else snprintf(err, errlen, "GPU tile sweep: %s", what);
+    }
+    return code;
 }
 
 // Z-slab part of one sweep: oriented c range of this slab and its inboxes.
@@ -1740,19 +1766,20 @@ inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int
     const int nJ = (B + ST_T - 1) / ST_T, nK = (ce - cs + ST_T - 1) / ST_T;
     const int ntasks = nJ * nK;
     const size_t nhb = (size_t)nJ * (ce - cs) * A;
-    if (W.cap_hb < nhb || W.cap_hc < (size_t)nK * B * A) (void)hipStreamSynchronize(st);
-    if (st_grow(&W.hb, &W.cap_hb, nhb, st)) return -5;
-    if (st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A, st)) return -5;
+    if (W.cap_hb < nhb || W.cap_hc < (size_t)nK * B * A)
+        if (int rc = st_sync(st)) return rc;
+    if (int rc = st_grow(&W.hb, &W.cap_hb, nhb, st)) return rc;
+    if (int rc = st_grow(&W.hc, &W.cap_hc, (size_t)nK * B * A, st)) return rc;
     if (!W.ctrl) {
-        if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return -5;
-        if (hipMalloc((void **)&W.stats, ST_NSTATS * sizeof(unsigned long long)) != hipSuccess) return -5;
-        if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return -4;
+        if (hipError_t e = hipMalloc((void **)&W.ctrl, 16 * sizeof(int)); e != hipSuccess) return sdf_hip_rc(e);
+        if (hipError_t e = hipMalloc((void **)&W.stats, ST_NSTATS * sizeof(unsigned long long)); e != hipSuccess) return sdf_hip_rc(e);
+        if (hipError_t e = hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st); e != hipSuccess) return sdf_hip_rc(e);
     }
     int ti = (W.task_nJ[0] == nJ && W.task_nK[0] == nK) ? 0 : (W.task_nJ[1] == nJ && W.task_nK[1] == nK) ? 1 : -1;
     if (ti < 0) {
         ti = W.task_next;
         W.task_next ^= 1;
-        (void)hipStreamSynchronize(st);   // the slot being replaced may still be read by a running launch
+        if (int rc = st_sync(st)) return rc;   // the slot being replaced may still be read by a running launch
         std::vector<int2> t;
         t.reserve(ntasks);
         for (int d = 0; d <= nJ + nK - 2; ++d)
@@ -1764,17 +1791,55 @@ inline int st_prepare(TileSweepWorkspace &W, hipStream_t st, int ni, int nj, int
             if (W.tasks[ti]) (void)hipFree(W.tasks[ti]);
             W.tasks[ti] = nullptr;
             W.cap_tasks[ti] = 0;
-            if (hipMalloc((void **)&W.tasks[ti], std::max(ntasks, 1) * sizeof(int2)) != hipSuccess) return -5;
+            if (hipError_t e = hipMalloc((void **)&W.tasks[ti], std::max(ntasks, 1) * sizeof(int2)); e != hipSuccess) {
+                W.tasks[ti] = nullptr;
+                return sdf_hip_rc(e);
+            }
             W.cap_tasks[ti] = std::max(ntasks, 1);
         }
-        if (ntasks && (hipMemcpyAsync(W.tasks[ti], t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice, st) != hipSuccess ||
-                       hipStreamSynchronize(st) != hipSuccess))
-            return -4;
+        if (ntasks) {
+            hipError_t e = hipMemcpyAsync(W.tasks[ti], t.data(), ntasks * sizeof(int2), hipMemcpyHostToDevice, st);
+            if (e == hipSuccess) e = hipStreamSynchronize(st);
+            if (e != hipSuccess) return sdf_hip_rc(e);
+        }
         W.task_nJ[ti] = nJ;
         W.task_nK[ti] = nK;
     }
     *ti_out = ti;
     return 0;
+}
+
+// Resident workgroups of k_sweep_tile<cfg> on the current device (occupancy query x CUs).
+template <class Cfg, bool SLAB, bool MULTI>
+inline int st_resident_cfg()
+{
+    int occ = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)k_sweep_tile<Cfg, SLAB, false, MULTI>, Cfg::THREADS, 0) !=
+            hipSuccess ||
+        hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
+        (void)hipGetLastError();
+        return 768;
+    }
+    return occ * cus;
+}
+// A slab's persistent tile grid when `share` slab sessions run on this device: half of the chip's resident
+// workgroups of that configuration split between them (share 8, quad tiles: 48 each), so every slab keeps
+// workgroups resident -- a slab waiting on its upstream neighbour must not hold the CUs that neighbour
+// needs -- with room left for the other slabs' second-pass kernels and for uneven placement.
+template <bool SLAB, bool MULTI>
+inline int st_share_grid(int cfg, int share)
+{
+    int r;
+    if (cfg == ST_CFG_THR) r = st_resident_cfg<StCfgThr, SLAB, MULTI>();
+    else if (cfg == ST_CFG_QUAD) r = st_resident_cfg<StCfgQuad, SLAB, MULTI>();
+    else if (cfg == ST_CFG_DUO) r = st_resident_cfg<StCfgDuo, SLAB, MULTI>();
+    else if (cfg == ST_CFG_OCT) r = st_resident_cfg<StCfgOct, SLAB, MULTI>();
+    else if (cfg == ST_CFG_QFP) {
+        if constexpr (MULTI) r = st_resident_cfg<StCfgQfp, SLAB, MULTI>();
+        else r = st_resident_cfg<StCfgQuad, SLAB, MULTI>();   // (st_launch: the quad tiles serve it)
+    }
+    else r = st_resident_cfg<StCfgLat, SLAB, MULTI>();
+    return std::max(8, r / (2 * std::max(share, 1)));
 }
 
 // Launch k_sweep_tile with the configuration `cfg` selects (st_cfg: ST_CFG_*), its lead cap applied.
@@ -1804,7 +1869,15 @@ inline void st_launch(int cfg, int grid, hipStream_t st, StParams &P, int lead_o
         // (the per-sweep launch of the fixed quad lanes crashed hipcc 7.2's greedy register allocator:
         // the quad tiles serve it)
         if constexpr (MULTI) st_launch_cfg<StCfgQfp, SLAB, TRACE, MULTI>("qfp", grid, st, P, lead_override);
-        else st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
+        else {
+            static bool told = false;   // say so once: a per-sweep launch asked for qfp runs the quad tiles
+            if (!told) {
+                told = true;
+                fprintf(stderr, "sdfgen: SDFGEN_TILE_CFG=5 (qfp) exists only for the one-launch first pass; "
+                                "this per-sweep tile launch runs the quad tiles\n");
+            }
+            st_launch_cfg<StCfgQuad, SLAB, TRACE, MULTI>("quad", grid, st, P, lead_override);
+        }
     }
     else st_launch_cfg<StCfgLat, SLAB, TRACE, MULTI>("lat", grid, st, P, lead_override);
 }
@@ -1818,14 +1891,12 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     const int cs = slab.on ? slab.cs : 0, ce = slab.on ? slab.ce : C;
     const int nJ = (B + ST_T - 1) / ST_T, nK = (ce - cs + ST_T - 1) / ST_T;
     const int ntasks = nJ * nK;
-    auto fail = [&](int code, const char *msg) {
-        if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
-        return code;
-    };
+    sdf_last_hip = hipSuccess;
+    auto fail = [&](int code, const char *msg) { return st_fail_msg(err, errlen, code, msg); };
     int ti = -1;
-    if (int rc = st_prepare(W, st, ni, nj, cs, ce, &ti)) return fail(rc, "buffer or task table allocation failed");
+    if (int rc = st_prepare(W, st, ni, nj, cs, ce, &ti)) return fail(rc, "buffer or task table set-up");
     if (++W.epoch == 0) ++W.epoch;   // 0 = never published
-    if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+    if (hipError_t e = zero_async(W.ctrl, sizeof(int), st); e != hipSuccess) return fail(sdf_hip_rc(e), "control word reset");
     StParams P;
     memset(&P, 0, sizeof(P));   // every field this launch does not use is null / 0 (P.tm was not: the
                                 // Z-slab launches then added their timers through a stray pointer)
@@ -1839,7 +1910,7 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.stats = W.count ? W.stats : nullptr;
     P.trace = nullptr;
     if (W.trace_sweep >= 0 && W.trace_sweep == W.cur_sweep) {
-        if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(-5, "trace");
+        if (int rc = st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(rc, "trace buffer");
         P.trace = W.trace;
     }
     P.ox = origin[0];
@@ -1884,12 +1955,13 @@ inline int tile_sweep(TileSweepWorkspace &W, hipStream_t st, const float4 *soup,
     P.tm = slab.on ? W.tm : nullptr;
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
-    if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
     const int cfg = st_cfg(ntasks);
+    if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
+    else if (W.grid_override <= 0 && W.share > 1 && slab.on) grid = std::min(grid, st_share_grid<true, false>(cfg, W.share));
     if (slab.on) st_launch<true, false, false>(cfg, grid, st, P, W.lead_override);
     else if (P.trace) st_launch<false, true, false>(cfg, grid, st, P, W.lead_override);
     else st_launch<false, false, false>(cfg, grid, st, P, W.lead_override);
-    if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return fail(sdf_hip_rc(e), "launch");
     return 0;
 }
 
@@ -1957,10 +2029,8 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
 {
     const int A = ni - 1, B = nj - 1, C = nk - 1;
     const int nJ = (B + ST_T - 1) / ST_T;
-    auto fail = [&](int code, const char *msg) {
-        if (err && errlen) snprintf(err, errlen, "GPU tile sweep: %s", msg);
-        return code;
-    };
+    sdf_last_hip = hipSuccess;
+    auto fail = [&](int code, const char *msg) { return st_fail_msg(err, errlen, code, msg); };
     StSlabPlan one;
     if (!plan) {
         one.kb = {0, nk};
@@ -1985,13 +2055,17 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     }
     nhb = std::max<size_t>(nhb, 1);
     nhc = std::max<size_t>(nhc, 1);
-    if (W.cap_mhb < ns * nhb || W.cap_mhc < ns * nhc) (void)hipStreamSynchronize(st);
-    if (st_grow(&W.mhb, &W.cap_mhb, ns * nhb, st)) return fail(-5, "halo buffer allocation failed");
-    if (st_grow(&W.mhc, &W.cap_mhc, ns * nhc, st)) return fail(-5, "halo buffer allocation failed");
+    // (the sync's status is checked: a fault of an earlier kernel on the stream -- the band, a previous
+    // call -- is sticky and must be reported as that fault, not as the allocation after it failing)
+    if (W.cap_mhb < ns * nhb || W.cap_mhc < ns * nhc)
+        if (int rc = st_sync(st)) return fail(rc, "stream sync before growing the halo buffers (an earlier kernel failed)");
+    if (int rc = st_grow(&W.mhb, &W.cap_mhb, ns * nhb, st)) return fail(rc, "halo buffer (b edges)");
+    if (int rc = st_grow(&W.mhc, &W.cap_mhc, ns * nhc, st)) return fail(rc, "halo buffer (c edges)");
     if (!W.ctrl) {
-        if (hipMalloc((void **)&W.ctrl, 16 * sizeof(int)) != hipSuccess) return fail(-5, "control allocation failed");
-        if (hipMalloc((void **)&W.stats, ST_NSTATS * sizeof(unsigned long long)) != hipSuccess) return fail(-5, "stats");
-        if (hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+        if (hipError_t e = hipMalloc((void **)&W.ctrl, 16 * sizeof(int)); e != hipSuccess) return fail(sdf_hip_rc(e), "control words");
+        if (hipError_t e = hipMalloc((void **)&W.stats, ST_NSTATS * sizeof(unsigned long long)); e != hipSuccess)
+            return fail(sdf_hip_rc(e), "statistics words");
+        if (hipError_t e = hipMemsetAsync(W.ctrl, 0, 16 * sizeof(int), st); e != hipSuccess) return fail(sdf_hip_rc(e), "control word reset");
     }
     int ntasks = 0;
     for (int q = 0; q < ns; ++q) ntasks += nJ * nKq[(size_t)q * nsl + me];
@@ -1999,7 +2073,7 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     key = key * 131 + nsl * 17 + me;
     if (const char *e = getenv("SDFGEN_TILE_WC")) key ^= (long long)(atof(e) * 1000.0) << 50;
     if (W.mkey != key) {
-        (void)hipStreamSynchronize(st);   // the tables may still be read by a running launch
+        if (int rc = st_sync(st)) return fail(rc, "stream sync before the task graph upload (an earlier kernel failed)");
         // Global tile ids: sweep q, slab r, tile (J, K).  Estimated starts (in units of one tile
         // hop = ST_T steps): +1 per upstream tile of the same sweep (across slab boundaries too),
         // + the tile duration after each previous-sweep tile of the same slab it waits for.
@@ -2098,26 +2172,22 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
             if (hipMalloc((void **)&W.mtasks, std::max(ntasks, 1) * sizeof(int4)) != hipSuccess ||
                 hipMalloc((void **)&W.mdeps, (size_t)std::max(ntasks, 1) * ST_MAXDEP * sizeof(int)) != hipSuccess ||
                 hipMalloc((void **)&W.mdone, std::max(ntasks, 1) * sizeof(unsigned)) != hipSuccess)
-                return fail(-5, "task graph allocation failed");
-            if (hipMemsetAsync(W.mdone, 0, std::max(ntasks, 1) * sizeof(unsigned), st) != hipSuccess)
-                return fail(-4, "memset");
+                return fail(sdf_hip_rc(hipGetLastError()), "task graph allocation");
+            if (hipError_t e = hipMemsetAsync(W.mdone, 0, std::max(ntasks, 1) * sizeof(unsigned), st); e != hipSuccess)
+                return fail(sdf_hip_rc(e), "completion flag reset");
             W.cap_mtasks = std::max(ntasks, 1);
         }
         if (ntasks) {
             hipError_t e = hipMemcpyAsync(W.mtasks, mt.data(), ntasks * sizeof(int4), hipMemcpyHostToDevice, st);
             if (e == hipSuccess) e = hipMemcpyAsync(W.mdeps, md.data(), md.size() * sizeof(int), hipMemcpyHostToDevice, st);
             if (e == hipSuccess) e = hipStreamSynchronize(st);
-            if (e != hipSuccess) {
-                char m[96];
-                snprintf(m, sizeof(m), "task graph upload: %s", hipGetErrorName(e));
-                return fail(-4, m);
-            }
+            if (e != hipSuccess) return fail(sdf_hip_rc(e), "task graph upload");
         }
         W.mkey = key;
     }
     if (prepare_only) return 0;   // buffers and tables in place (Z-slabs: before anything is enqueued)
     if (++W.mepoch == 0) ++W.mepoch;   // completion flags of this launch (0 = never)
-    if (zero_async(W.ctrl, sizeof(int), st) != hipSuccess) return fail(-4, "memset");
+    if (hipError_t e = zero_async(W.ctrl, sizeof(int), st); e != hipSuccess) return fail(sdf_hip_rc(e), "control word reset");
     StParams P;
     memset(&P, 0, sizeof(P));
     P.soup = soup;
@@ -2192,18 +2262,19 @@ inline int tile_sweep_multi(TileSweepWorkspace &W, hipStream_t st, const float4 
     }
     if (ntasks <= 0) return 0;
     int grid = ntasks < 2048 ? ntasks : 2048;
-    if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
     // configuration by this slab's tiles per sweep (the largest sweep of the launch)
     int tiles = 0;
     for (int q = 0; q < ns; ++q) tiles = std::max(tiles, nJ * nKq[(size_t)q * nsl + me]);
     W.cfg = st_cfg(tiles);
+    if (W.grid_override > 0 && W.grid_override < grid) grid = W.grid_override;
+    else if (W.grid_override <= 0 && W.share > 1 && nsl > 1) grid = std::min(grid, st_share_grid<true, true>(W.cfg, W.share));
     if (nsl > 1) st_launch<true, false, true>(W.cfg, grid, st, P, W.lead_override);
     else if (W.trace_multi) {   // diagnostics: per-task timeline of the whole launch (tools/trace_multi.py)
-        if (st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(-5, "trace");
+        if (int rc = st_grow(&W.trace, &W.cap_trace, 8 * (size_t)ntasks, st)) return fail(rc, "trace buffer");
         P.trace = W.trace;
         st_launch<false, true, true>(W.cfg, grid, st, P, W.lead_override);
     } else st_launch<false, false, true>(W.cfg, grid, st, P, W.lead_override);
-    if (hipGetLastError() != hipSuccess) return fail(-4, "launch failed");
+    if (hipError_t e = hipGetLastError(); e != hipSuccess) return fail(sdf_hip_rc(e), "launch");
     return 0;
 }
 

@@ -50,7 +50,7 @@ def test_build_id_matches_sources():
 
 
 def test_abi_version_and_device_count():
-    assert _lib.lib.sdfgen_hip_abi_version() == 4
+    assert _lib.lib.sdfgen_hip_abi_version() == 5
     assert _lib.device_count() >= 0
 
 

@@ -307,3 +307,18 @@ def test_embedded_x3y4z5_mesh_matches_the_stl_file():
     ev, et = meshgen.x3y4z5()
     assert ev.dtype == np.float32 and et.dtype == np.uint32
     assert np.array_equal(ev, np.asarray(v, np.float32)) and np.array_equal(et, np.asarray(t, np.uint32))
+
+
+def test_sdfgen_ngpu_env_parsing(monkeypatch):
+    """generate_sdf's GPU-count knob (SDFGEN_NGPU) parses like the C++ drop-in's ngpu_from_env."""
+    import sdfgenfast_amd as S
+    from sdfgenfast_amd import _lib
+    for val, want in (("", _lib.NGPU_CURRENT), ("1", 1), ("all", _lib.NGPU_ALL), ("0", 0), ("8", 8)):
+        monkeypatch.setenv("SDFGEN_NGPU", val)
+        assert S._ngpu_from_env() == want, val
+    monkeypatch.delenv("SDFGEN_NGPU")
+    assert S._ngpu_from_env() == _lib.NGPU_CURRENT
+    for bad in ("two", "-1", "2.5"):
+        monkeypatch.setenv("SDFGEN_NGPU", bad)
+        with pytest.raises(ValueError):
+            S._ngpu_from_env()

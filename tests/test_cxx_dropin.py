@@ -136,3 +136,36 @@ def test_gpu_cxx_caller_matches_fixture(name, tmp_path):
     case = CASES[name]
     for mode in ("gpu", "gpu-direct", "auto"):
         assert bits_equal(run_caller(own_caller(), case, mode, tmp_path), case.phi), (name, mode)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ngpu", ["2", "all"])
+def test_gpu_cxx_caller_sdfgen_ngpu_knob(ngpu, tmp_path):
+    """SDFGEN_NGPU, the drop-in's GPU-count knob (the reference signature has no device argument,
+    common/sdfgen_unified.h:47-57): the C++ caller, unchanged, splits the grid into Z-slabs -- here two
+    slab sessions on this box's one GPU (SDFGEN_DEBUG_SLABS_ONE_DEVICE; 'all' is the one device, so one
+    slab) -- bit-exact against the reference fixture."""
+    case = CASES["sphere3600_40x44x52"]
+    env = dict(os.environ, SDFGEN_NGPU=ngpu, SDFGEN_DEBUG_SLABS_ONE_DEVICE="1", GPU_MAX_HW_QUEUES="8")
+    mesh, out = str(tmp_path / "m.mesh"), str(tmp_path / "m.phi")
+    write_mesh(mesh, case)
+    for mode in ("gpu", "gpu-direct"):
+        r = subprocess.run([own_caller(), mesh, mode, out], capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stdout + r.stderr
+        ni, nj, nk = case.dims
+        got = np.fromfile(out, np.float32).reshape(nk, nj, ni).transpose(2, 1, 0)
+        assert bits_equal(got, case.phi), (ngpu, mode)
+
+
+def test_cxx_sdfgen_ngpu_rejects_garbage(tmp_path):
+    """A malformed SDFGEN_NGPU is std::invalid_argument from the GPU drop-in (checked before any
+    device work; on a box without a GPU the 'no GPU' error comes first, which is also an error)."""
+    case = CASES["cube_tiny_1x5x4"]
+    mesh, out = str(tmp_path / "m.mesh"), str(tmp_path / "m.phi")
+    write_mesh(mesh, case)
+    env = dict(os.environ, SDFGEN_NGPU="two")
+    r = subprocess.run([own_caller(), mesh, "gpu", out], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    # the CPU backend ignores the knob
+    r = subprocess.run([own_caller(), mesh, "cpu", out], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr

@@ -95,3 +95,16 @@ def test_bounds_one_gpu_sweep_paths(mode):
     r = subprocess.run([sys.executable, "-c", code], env=_env(**env), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert r.stdout.split()[0] == "OK" and r.stdout.split()[1] == BOUNDS_LIB, r.stdout
+
+
+def test_bounds_band_sign_prep_kernels():
+    """k_prep_soup, k_band_lds, k_band_big, the ray-parity counts, k_sign and k_sign_kfast on the bounds
+    build (SDF_CHK sites 40-50): the golden and edge fixtures' stage 1 against oracle.band and their whole
+    calls in both layouts against the reference's output, plus coarse soups through the big-triangle list.
+    A wrong pair -> triangle search (the round-5 half-wave ballot build) now fails as a named site here,
+    not as a GPU fault that surfaces later as a failed allocation."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "band_bounds_check.py")], env=_env(),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    last = r.stdout.strip().splitlines()[-1].split()
+    assert last[0] == "OK" and last[1] == BOUNDS_LIB, r.stdout[-3000:]

@@ -37,6 +37,13 @@ def _worker(rank, world, port, dims, result_path):
             np.save(result_path, np.asfortranarray(phi))
         dist.barrier()
         D.release()
+        if rank == 0:
+            # a one-GPU call after release() in a process that held IPC imports of the peer's blocks (ADVICE
+            # r05: release keeps those mappings and the block pool, so no later allocation lands on them)
+            from sdfgenfast_amd import _lib
+            _lib.release()
+            np.save(result_path + ".after.npy",
+                    np.asfortranarray(_lib.make_level_set3(v, t, o, dx, *dims, 1, _lib.LAYOUT_ARRAY3)))
     finally:
         dist.destroy_process_group()
 
@@ -50,6 +57,8 @@ def test_distributed_gpu_two_ranks_match_oracle(tmp_path, dims):
     want = np.asfortranarray(O.make_level_set3(v, t, o, dx, *dims, 1))
     got = np.load(path)
     assert bits_equal(got, want), diff_report(got, want, dx)
+    after = np.load(path + ".after.npy")
+    assert bits_equal(after, want), "one-GPU call after release: " + diff_report(after, want, dx)
 
 
 def _bench_two_ranks(*extra):

@@ -138,12 +138,16 @@ def test_eight_slabs_in_process_match_reference_digest(name, mode):
     one process -- every slab with both neighbours but the ends, seven slab boundaries per sweep --
     against the reference's SHA-256 of phi.  `slabs`: the slab C-ABI driven per slab (8 streams, one
     hardware queue each); `cabi`: sdfgen_hip_make_level_set3(ngpu=8), the library's own in-process
-    multi-device path, with SDFGEN_DEBUG_SLABS_ONE_DEVICE.  The persistent grids are capped so that
-    all eight slabs stay co-resident: 48 tile workgroups and 64 repair workgroups per slab (a slab's
-    repair kernel ends only after its upstream neighbour's, so all eight must be resident at once: 8 x
-    the default 256 one-wave repair workgroups at 171 VGPRs are exactly the chip's 2,048 wave slots for
-    them -- a first run without the cap ran into the repair watchdogs).  On 8 GPUs nothing is shared."""
-    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", SDFGEN_TILE_GRID="48", SDFGEN_SPARSE_WORKERS="64")
+    multi-device path, with SDFGEN_DEBUG_SLABS_ONE_DEVICE.  The LIBRARY caps the persistent grids so
+    that all eight slabs stay co-resident (no SDFGEN_TILE_GRID / SDFGEN_SPARSE_WORKERS here): it counts
+    the slab sessions alive on the device and gives each half of the tile kernel's resident workgroups
+    / 8 and a quarter of the repair kernel's / 8 (a slab's repair kernel ends only after its upstream
+    neighbour's, so all eight must be resident at once: 8 x the default 256 one-wave repair workgroups
+    at 171 VGPRs are exactly the chip's 2,048 wave slots for them -- a round-5 run without a cap ran into
+    the repair watchdogs).  One hardware queue per slab stream (GPU_MAX_HW_QUEUES; the library refuses
+    more sessions on a device than queues).  On 8 GPUs nothing is shared."""
+    env = {k: v for k, v in os.environ.items() if k not in ("SDFGEN_TILE_GRID", "SDFGEN_SPARSE_WORKERS")}
+    env["GPU_MAX_HW_QUEUES"] = "16"
     args = ["8", name, "2" if name.startswith("c2") else "1"] + (["--cabi"] if mode == "cabi" else [])
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "slab_inprocess_check.py"), *args],
                        env=env, capture_output=True, text=True, timeout=600)
@@ -213,3 +217,24 @@ def test_c_abi_ngpu_all_means_every_visible_device():
     assert bits_equal(got_cur, want), diff_report(got_cur, want, dx)
     if _lib.device_count() == 1:
         assert _lib.last_profile()["sweep_impl"] != 3  # one device: not the slab path
+
+
+@pytest.mark.parametrize("ngpu", ["2"])   # (2 slabs: GPU_MAX_HW_QUEUES is 4 in this process, see above)
+def test_generate_sdf_sdfgen_ngpu_knob(ngpu, monkeypatch):
+    """SDFGEN_NGPU, the Python drop-in's GPU-count knob (generate_sdf keeps the reference signature,
+    python/sdfgen_py.cpp:160-218): the grid splits into Z-slabs, here sessions on this box's one GPU
+    (SDFGEN_DEBUG_SLABS_ONE_DEVICE) with the library's own grid caps (no SDFGEN_TILE_GRID), bit-exact
+    against the oracle; a malformed value is a ValueError."""
+    import sdfgenfast_amd as S
+    from sdfgenfast_amd import _lib
+    monkeypatch.delenv("SDFGEN_TILE_GRID", raising=False)
+    monkeypatch.setenv("SDFGEN_DEBUG_SLABS_ONE_DEVICE", "1")
+    monkeypatch.setenv("SDFGEN_NGPU", ngpu)
+    v, t, o, dx, dims = _mesh(dims=(37, 41, 46))
+    got = S.generate_sdf(v, t, o, dx, *dims, exact_band=1, backend="gpu")
+    assert _lib.last_profile()["slabs"] == int(ngpu)
+    want = np.asarray(O.make_level_set3(v, t, o, dx, *dims, 1))
+    assert bits_equal(got, want), diff_report(got, want, dx)
+    monkeypatch.setenv("SDFGEN_NGPU", "x2")
+    with pytest.raises(ValueError):
+        S.generate_sdf(v, t, o, dx, *dims, exact_band=1, backend="gpu")

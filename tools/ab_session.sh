@@ -8,6 +8,12 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=$1; shift
 lib() { [ "$1" = cur ] && echo "" || echo "ab/$1.so"; }   # "cur": the in-tree library
+# every library of the session must exist before anything runs (round 5 lost sessions to "ab/cur.so is
+# missing": a build that was never made, or "cur" spelled as a file)
+for v in "$@"; do
+  f=$([ "$v" = cur ] && echo sdfgenfast_amd/libsdfgen_hip.so || echo "ab/$v.so")
+  [ -f "$f" ] || { echo "ab_session: $f is missing -- build it first (tools/ab_build.sh); nothing run"; exit 2; }
+done
 cfgs=(); for v in "$@"; do cfgs+=("SDFGEN_LIB_OVERRIDE=$(lib $v)"); done
 for v in "$@"; do
   [ "$v" = cur ] && continue
