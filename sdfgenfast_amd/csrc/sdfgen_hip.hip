@@ -387,9 +387,10 @@ __global__ void __launch_bounds__(256, BAND_WPE) k_band_lds(const float4 *__rest
         __syncthreads();
         // (triangle, cell) pair of flat index fl (triangle q of the batch)
         auto pair_in = [&](int q, unsigned fl, int &i, int &j, int &k) {
-            // bounds builds: the pair's triangle is one of the batch's, and fl lies in its box
+            // bounds builds: the pair's triangle is one of the batch's, and a live pair's fl lies in its box
+            // (lanes past the batch's last pair decode one too, never emitted)
             q = (int)SDF_CHK(42, q, 0, nb);
-            (void)SDF_CHK(43, fl, s_pre[q], s_pre[q + 1]);
+            if (fl < total) (void)SDF_CHK(43, fl, s_pre[q], s_pre[q + 1]);
             const BandBox B = s_box[q];
             const unsigned r = fl - s_pre[q], bij = (unsigned)(B.bi * B.bj);
 #if BAND_FDIV
@@ -1999,12 +2000,21 @@ int run_zslab_local(const uint32_t *tri, uint64_t ntri, const float *xyz, uint64
                                     (size_t)ni * nj, hipMemcpyDeviceToHost, T->stream));
     }
     int first = 0;
+    sdfgen_hip_profile slowest;
+    memset(&slowest, 0, sizeof(slowest));
     for (int g = 0; g < n; ++g) {   // collect every slab's status, report the first failure
         Err e2{nullptr, 0};
         SlabSession *T = slab_of(S[g].h);
         HIPCHK(hipSetDevice(T->device));
-        rc = slab_finish(T, nvert, nullptr, first ? e2 : err);
+        sdfgen_hip_profile p;
+        memset(&p, 0, sizeof(p));
+        rc = slab_finish(T, nvert, &p, first ? e2 : err);
         if (rc && !first) first = rc;
+        if (!rc && (g == 0 || p.total_ms > slowest.total_ms)) slowest = p;
+    }
+    if (!first) {   // sdfgen_hip_last_profile of an ngpu > 1 call: the slowest slab's (its `slabs` = n)
+        std::lock_guard<std::mutex> lk(g_prof_mu);
+        g_prof = slowest;
     }
     return first;
 }
