@@ -108,8 +108,9 @@ static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: powe
 
 // Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, the waves
 // per SIMD the register budget must allow, and lanes per cell (4: quad lanes, 2: duo lanes).
-template <int NCW_, int RR_, bool TWIN_, int WPE_, int LPC_ = 1, bool FIX_ = false>
+template <int NCW_, int RR_, bool TWIN_, int WPE_, int LPC_ = 1, bool FIX_ = false, int NH_ = 1>
 struct StCfg {
+    static constexpr int NH = NH_;                      // helper waves: 1 (own data and halo), 2 (one each)
     static constexpr bool FIX = FIX_;                   // quad lanes with fixed slots (q = r, r + 4) in one packed pass
     static constexpr int NCW = NCW_;                    // compute waves per tile
     static constexpr int CLW = ST_T / NCW;              // c-columns per compute wave
@@ -121,7 +122,8 @@ struct StCfg {
     static constexpr int LPC_SH = LPC_ == 8 ? 3 : (LPC_ == 4 ? 2 : (LPC_ == 2 ? 1 : 0));
     static constexpr int WPE = WPE_;
     static constexpr int LEAD = NCW > 1 ? RR - 4 : 0;   // max lead of wave w over wave w+1 (ring hazard)
-    static constexpr int THREADS = 64 * (NCW + 1);      // compute waves + helper wave
+    static constexpr int THREADS = 64 * (NCW + NH);     // compute waves + helper wave(s)
+    static_assert(NH == 1 || NH == 2, "one helper wave, or an own-data and a halo helper");
     static constexpr int RING0 = 0;                                 // RR slots x 64 columns
     static constexpr int HALO0 = RING0 + RR * ST_NCOL;              // 17 streams x RH
     static constexpr int OWN0 = HALO0 + ST_NSTREAM * ST_RH;         // RO slots x 64 columns
@@ -160,7 +162,10 @@ using StCfgThr = StCfg<1, ST_THR_RR, false, ST_THR_WPE>;
 #ifndef ST_QUAD_WPE
 #define ST_QUAD_WPE 4
 #endif
-using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, 4>;
+#ifndef ST_QUAD_NH
+#define ST_QUAD_NH 1   // 2: the helper split into an own-data wave and a halo wave (6 waves per tile, 2 tiles per CU)
+#endif
+using StCfgQuad = StCfg<4, 8, false, ST_QUAD_WPE, 4, false, ST_QUAD_NH>;
 // Duo lanes (round 5): 2 compute waves of 32 cells, two lanes per cell -- lane 2x + r evaluates the
 // cell's candidates of rank r, r + 2, ... in passes of one ptd_wave each (a second pass only when a cell
 // of the wave has more than 2 candidates), a first-minimum reduction over the pair (one DPP move).  Half
@@ -527,7 +532,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 s_abort = 0;
                 s_halo_ready[ST_NSTREAM] = 0x3fffffff;
             }
-        } else if (L < ST_NSTREAM) {
+        } else if ((Cfg::NH == 1 || wave == ST_NCW) && L < ST_NSTREAM) {
             int hb_ = 0, hc_ = 0;
             bool valid;
             if (L < ST_T) { hb_ = b0 - 1; hc_ = c0 + L; valid = hc_ < P.ce; }
@@ -1397,12 +1402,19 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 }
             }
         } else {
+            // ======================= helper wave(s) =======================
+            // ROLE 0: the one helper wave (own data and halo); with Cfg::NH == 2 the first helper wave takes ROLE 1
+            // (own columns only) and the second ROLE 2 (halo streams only): each round trip then carries half the
+            // loads, and neither kind waits behind the other's gathers.  (A constant 0 with one helper: the role
+            // tests fold away and the code is the one-helper loop instruction for instruction -- a lambda per role
+            // cost the default build 2 % in register allocation, round 5.)
+            const int ROLE = Cfg::NH == 1 ? 0 : (wave == ST_NCW ? 1 : 2);
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
             const int bl = L & (ST_T - 1), cl = L >> 3;   // helper lane L prefetches column (bl, cl)
             const int b = b0 + bl, c = c0 + cl;
-            const bool col = b < P.B && c < P.ce;
-            // ======================= helper wave =======================
+            const bool col = ROLE != 2 && b < P.B && c < P.ce;
             // stream geometry (lanes < 17)
-            const bool hlane = L < ST_NSTREAM;
+            const bool hlane = ROLE != 1 && L < ST_NSTREAM;
             int hbs = 0, hcs = 0, hoff = 0;
             bool hvalid = false, hbound = true;
             const unsigned long long *hsrc = nullptr;
@@ -1443,7 +1455,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             // hot line for the whole chip (first pass 14.0 -> 13.9 ms at 256^3, 51.4 -> 50.6 ms at 512^3)
             // (0 when the triangle count is unknown: ntri is ~0 until a pipeline sets it)
             const int gdum = (P.ntri >= 1 && P.ntri < 0x7fffffffull) ? (int)((unsigned)(J * 40503 + K * 9973 + 17) % (unsigned)P.ntri) : 0;
-            int fA = 0, gA = 0;                    // own steps [fA, fA+gA) whose cells are in c0..c3
+            int fA = ROLE == 2 ? nsteps : 0, gA = 0;   // own steps [fA, fA+gA) whose cells are in c0..c3 (ROLE 2: none)
             int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
             unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
@@ -1500,22 +1512,17 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 const bool r3 = hbound || st_granule_ready(q3, P.epoch);
                 if (0 < hcA && r0) { hp = 1; if (1 < hcA && r1) { hp = 2; if (2 < hcA && r2) { hp = 3; if (3 < hcA && r3) hp = 4; } } }
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
+// (the role tests are conditional operators on ROLE, a constant with one helper wave: clang emits only the
+// live arm, so the one-helper code is the original's instruction for instruction)
 #define ST_GATHER(g, cg, qg)                                                                          \
     const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
-    const float4 oa##g = P.soup[so##g], ob##g = P.soup[so##g + 1], oc##g = P.soup[so##g + 2];          \
+    const float4 oa##g = ROLE != 2 ? P.soup[so##g] : z4, ob##g = ROLE != 2 ? P.soup[so##g + 1] : z4,    \
+                 oc##g = ROLE != 2 ? P.soup[so##g + 2] : z4;                                           \
     const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
-    const float4 ha##g = P.soup[sh##g], hb##g = P.soup[sh##g + 1], hc##g = P.soup[sh##g + 2];
+    const float4 ha##g = ROLE != 1 ? P.soup[sh##g] : z4, hb##g = ROLE != 1 ? P.soup[sh##g + 1] : z4,    \
+                 hc##g = ROLE != 1 ? P.soup[sh##g + 2] : z4;
                 ST_GATHER(0, c0, q0)
-#ifdef ST_OWNDEDUP   // experiment: slot 1 repeating slot 0's label reads the shared dummy line instead
-                const bool dup1 = ST_OWN_OK(0) && ST_OWN_OK(1) && lbl_of((uint32_t)c1) == lbl_of((uint32_t)c0);
-                const bool hdup1 = 0 < hp && 1 < hp && lbl_of((uint32_t)q1) == lbl_of((uint32_t)q0);
-                const size_t so1 = 3 * SDF_CHK(11, (ST_OWN_OK(1) && !dup1 && lbl_of((uint32_t)c1) >= 0 ? lbl_of((uint32_t)c1) : gdum), 0, P.ntri);
-                const float4 oa1_ = P.soup[so1], ob1_ = P.soup[so1 + 1], oc1_ = P.soup[so1 + 2];
-                const size_t sh1 = 3 * SDF_CHK(12, (1 < hp && !hdup1 && lbl_of((uint32_t)q1) >= 0 ? lbl_of((uint32_t)q1) : gdum), 0, P.ntri);
-                const float4 ha1_ = P.soup[sh1], hb1_ = P.soup[sh1 + 1], hc1_ = P.soup[sh1 + 2];
-#else
                 ST_GATHER(1, c1, q1)
-#endif
 #if ST_G_DEF > 2
                 ST_GATHER(2, c2, q2)
                 ST_GATHER(3, c3, q3)
@@ -1535,11 +1542,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
         const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
-        cn = P.cell[SDF_CHK(6, ix_, P.clo, P.chi)];                                                    \
+        cn = ROLE != 2 ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;                               \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
                        : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + hB + (g)); \
-        qn = __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE);                                        \
+        qn = ROLE != 1 ? __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE) : 0ull;                      \
     }
                 // Always issued (a fixed count keeps the waits below precise); slots with nothing
                 // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
@@ -1572,15 +1579,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         s_ent[3 * e_ + 2] = hc##g;                                                                     \
     }
                 ST_LAND(0, c0, q0)
-#ifdef ST_OWNDEDUP
-                {
-                    const float4 oa1 = dup1 ? oa0 : oa1_, ob1 = dup1 ? ob0 : ob1_, oc1 = dup1 ? oc0 : oc1_;
-                    const float4 ha1 = hdup1 ? ha0 : ha1_, hb1 = hdup1 ? hb0 : hb1_, hc1 = hdup1 ? hc0 : hc1_;
-                    ST_LAND(1, c1, q1)
-                }
-#else
                 ST_LAND(1, c1, q1)
-#endif
 #if ST_G_DEF > 2
                 ST_LAND(2, c2, q2)
                 ST_LAND(3, c3, q3)
@@ -1641,7 +1640,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 atomicAdd(P.stats + 19, hp_halo);
             }
 #endif
-            if (SLAB && P.tm && L == 0) {   // where the slab boundary's tiles wait for the upstream GPU
+            if (SLAB && P.tm && L == 0 && ROLE != 1) {   // where the slab boundary's tiles wait for the upstream GPU
                 atomicAdd(P.tm + (inbox ? TM_INBOX_IDLE : TM_OTHER_IDLE), t_idle);
                 atomicAdd(P.tm + (inbox ? TM_INBOX_TASKS : TM_OTHER_TASKS), 1ull);
             }
