@@ -115,6 +115,52 @@ def chain_model(ni, nj, nk, nslabs, nsw=8):
     return (max(kv.values()) + wc) * ST_T
 
 
+def gs_levels(ni, nj, nk, nsw=8):
+    """The exact critical path of the reference's first pass at CELL granularity, in levels: node (sweep s,
+    cell p) depends on (s, its upwind neighbours) and on (s - 1, p) (cpu_lib/makelevelset3.cpp:243-291,
+    130-151).  The diagonal neighbours never lengthen it, so L_s(p) = 1 + max(L_{s-1}(p), L_s(p - e_x) for the
+    three axes x), i.e. a running maximum with +1 per cell along each axis in the sweep's direction.  No
+    schedule and no GPU count can run the first pass in fewer dependent steps at parity."""
+    import numpy as np
+    A, B, C = ni - 1, nj - 1, nk - 1   # oriented cells per axis (the boundary planes are fixed)
+    L = np.zeros((A, B, C), np.int32)
+    idx = [np.arange(n, dtype=np.int32).reshape(sh) for n, sh in
+           ((A, (A, 1, 1)), (B, (1, B, 1)), (C, (1, 1, C)))]
+    for q in range(nsw):
+        d = DIRS[q % 8]
+        L += 1
+        for ax in range(3):
+            v = L if d[ax] > 0 else np.flip(L, axis=ax)
+            v -= idx[ax]
+            np.maximum.accumulate(v, axis=ax, out=v)
+            v += idx[ax]
+    return int(L.max())
+
+
+def ceiling(name, inp, steps_us=(1.088, 0.75, 0.49, 0.38), n=8):
+    """the N-GPU efficiency this design could reach with a shorter isolated step.  First
+    pass = max(levels x s, work / N) (crowding as in predict); second pass with the measured repair (does
+    not shrink with N) and with every repair link at its idle-chip latency (the best case)."""
+    ni, nj, nk = inp["dims"]
+    lv = gs_levels(ni, nj, nk)
+    base = predict(name, inp, (1,))["rows"][0]["total_ms"]
+    c1 = chain_model(ni, nj, nk, 1) * S_ISO_US * 1e-3
+    crowd = inp["t_first"] / max(c1, inp["t_first_work"])
+    t_scan = inp["t_second"] / 8 - inp["t_repair_per_sweep"]
+    hand = (2 * H_FLAG_US + (n - 1) * H_X_US) * 1e-3
+    rows = []
+    for s in steps_us:
+        first = max(lv * s * 1e-3 + 8 * (n - 1) * H_X_US * 1e-3, inp["t_first_work"] / n) * (1.0 + (crowd - 1.0) / n)
+        sec_hi = 8 * (t_scan / n + inp["t_repair_per_sweep"] + hand)
+        sec_lo = 8 * (t_scan / n + min(inp["t_repair_per_sweep"], inp["longest_chain"] * LINK_IDLE_US * 1e-3) + hand)
+        local = inp["t_local"] / n
+        rows.append({"step_us": s, "gs_levels": lv, "first_ms": round(first, 3), "second_ms": round(sec_hi, 3),
+                     "second_ms_links_idle": round(sec_lo, 3),
+                     "efficiency": round(base / (n * (local + first + sec_hi)), 3),
+                     "efficiency_links_idle": round(base / (n * (local + first + sec_lo)), 3)})
+    return rows
+
+
 def predict(name, inp, ns=(1, 2, 4, 8)):
     ni, nj, nk = inp["dims"]
     c1 = chain_model(ni, nj, nk, 1)
@@ -189,6 +235,8 @@ def main():
             print("  ", json.dumps(r))
         for r in predict_schedules(name, inp):
             print("   schedule", json.dumps(r))
+        for r in ceiling(name, inp):
+            print("   ceiling n=8", json.dumps(r))
 
 
 if __name__ == "__main__":
