@@ -978,7 +978,7 @@ int run_pipeline(Workspace *ws, hipStream_t st, const uint32_t *d_tri, uint64_t 
 {
     const uint64_t n = (uint64_t)ni * nj * nk;
     int rc;
-    if ((rc = grow(&ws->cell, &ws->cap_cell, n, err))) return rc;
+    if ((rc = grow(&ws->cell, &ws->cap_cell, sp_pad(n), err))) return rc;   // (k_sp_jscan2 reads past the last cell)
     if ((rc = grow(&ws->cnt, &ws->cap_cnt, n, err))) return rc;
     if ((rc = grow(&ws->soup, &ws->cap_soup, 3 * std::max<uint64_t>(ntri, 1), err))) return rc;
     if (!ws->err_flag) {
@@ -2148,7 +2148,7 @@ int sdfgen_hip_debug_band(const uint32_t *tri, uint64_t ntri, const float *xyz, 
     const uint64_t n = (uint64_t)ni * nj * nk;
     if ((rc = grow(&ws->tri, &ws->cap_tri, std::max<uint64_t>(3 * ntri, 1), err))) return rc;
     if ((rc = grow(&ws->xyz, &ws->cap_xyz, std::max<uint64_t>(3 * nvert, 1), err))) return rc;
-    if ((rc = grow(&ws->cell, &ws->cap_cell, n, err))) return rc;
+    if ((rc = grow(&ws->cell, &ws->cap_cell, sp_pad(n), err))) return rc;   // (k_sp_jscan2 reads past the last cell)
     if ((rc = grow(&ws->cnt, &ws->cap_cnt, n, err))) return rc;
     if ((rc = grow(&ws->soup, &ws->cap_soup, 3 * std::max<uint64_t>(ntri, 1), err))) return rc;
     if (!ws->err_flag) {

@@ -145,6 +145,10 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
 #define SP_JSCAN_FAST 1   // k_sp_jacobi on one device below 2^29 cells: scalar neighbour bases, one 32-bit offset, and
                           // only "any candidate" (sp_any_scan) -- the scan is VALU-issue-bound since SP_VMASK
 #endif
+#ifndef SP_JSCAN_PAIR
+#define SP_JSCAN_PAIR 1   // the fast scan as k_sp_jscan2: two cells per lane, 16-byte loads (needs 2 cells of padding
+                          // past the grid in both state buffers: sp_pad)
+#endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
@@ -792,6 +796,150 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
         if (f) buf[cnt + __builtin_popcountll(want & ((1ull << lane) - 1ull))] = c32;
         cnt += (unsigned)__builtin_popcountll(want);
         if (cnt > SP_JWAVE - 64) {
+            sp_jlist_flush(P, part, buf, cnt, lane);
+            cnt = 0;
+        }
+        i += si;
+        const int ci = i >= P.ni;
+        i -= ci ? P.ni : 0;
+        j += sj + ci;
+        const int cj = j >= P.nj;
+        j -= cj ? P.nj : 0;
+        k += sk + cj;
+    }
+    if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
+}
+
+// The fast scan with 16-byte loads (SP_JSCAN_PAIR).  The scan's limiter is the texture addresser: TA busy
+// 82 % (average over the chip's TA units, 96 % at the busiest) of the C4 launch's cycles while HBM ran at
+// 2.8 TB/s and VALU issue at ~18 % (profiles/r06_limiter_c4.json); a wave-wide load costs the TA about the same
+// per lane whatever its width (MI355X_MICROARCH.md: 8-B accesses 0.54-0.70x the 16-B rate), and k_sp_jacobi
+// issued 8 of them per 64 cells: the cell (8 B) and its 7 upwind low words (4 B each).  Here a lane holds
+// two consecutive cells (c, c + 1) and loads four 16-byte pairs -- its own, the j-upwind row's, the
+// k-upwind plane's and the jk-diagonal's -- which hold every upwind word of both cells except the
+// i-direction ones of one cell: those are the neighbouring lane's pair elements, moved by DPP (wave_shr:1 for
+// di > 0, wave_shl:1 for di < 0; the wave's edge lane loads its four words itself).  4 wide loads per 128
+// cells instead of 16 narrow ones.  Lanes whose pairs would leave the grid (its first planes / rows, and the
+// last for negative directions) fill the pair registers word by word with bounds checks instead, so the DPP
+// sources are right for every cell that needs them (a cell of the sweep's range has all its upwind words
+// in the grid).  Same traversal (XCD eighths, one contiguous chunk per block), same list order (cells in
+// address order), same decision (sp_any_scan): the list equals k_sp_jacobi<false, true>'s.
+typedef uint32_t sp_u32x4 __attribute__((ext_vector_type(4), aligned(8)));   // two 8-byte cells, 8-byte aligned
+constexpr unsigned long long SP_PAD = 2;   // cells of padding past n in the state buffers (sp_pad)
+inline unsigned long long sp_pad(unsigned long long n) { return n + SP_PAD; }
+
+__global__ void __launch_bounds__(256) k_sp_jscan2(SpParams P)
+{
+    __shared__ unsigned s_list[4][SP_JWAVE];
+    const unsigned lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD
+    unsigned *buf = s_list[wv];
+    unsigned cnt = 0;   // wave-uniform
+    const unsigned long long span = (P.n + 7) / 8;   // launched with gridDim.x % 8 == 0 (sp_launch_jacobi)
+    const unsigned long long base = (unsigned long long)(blockIdx.x % 8) * span;
+    const unsigned long long nb = gridDim.x / 8;
+    const unsigned long long chunk = (span + nb * blockDim.x - 1) / (nb * blockDim.x) * blockDim.x;
+    const unsigned long long c_beg = (unsigned long long)(blockIdx.x / 8) * chunk;
+    const unsigned long long c_end = std::min(span, c_beg + chunk);
+    // an iteration covers 512 cells of the chunk: wave wv the 128 from wv * 128, lane L two of them
+    const unsigned long long first = c_beg + wv * 128u + 2u * lane;
+    constexpr unsigned STEP = 512;
+    int i, j, k, si, sj, sk;
+    {
+        const unsigned c0 = (unsigned)(base + first), r0 = c0 / (unsigned)P.ni;
+        i = (int)(c0 % (unsigned)P.ni);
+        j = (int)(r0 % (unsigned)P.nj);
+        k = (int)(r0 / (unsigned)P.nj);
+        const unsigned rs = STEP / (unsigned)P.ni;
+        si = (int)(STEP % (unsigned)P.ni);
+        sj = (int)(rs % (unsigned)P.nj);
+        sk = (int)(rs / (unsigned)P.nj);
+    }
+    const long long dJ = -(long long)P.dj * P.ni, dK = -(long long)P.dk * P.ni * P.nj;   // pair offsets (cells)
+    const long long dlo = std::min(dJ, 0ll) + std::min(dK, 0ll), dhi = std::max(dJ, 0ll) + std::max(dK, 0ll);
+    const char *bS = (const char *)P.S, *bJ = (const char *)(P.S + dJ), *bK = (const char *)(P.S + dK),
+               *bJK = (const char *)(P.S + dJ + dK);   // (scalar bases; a base may lie outside the buffer)
+    const bool pos = P.di > 0;
+    const long long dI = pos ? -1 : 2;   // the edge lane's own fetch: cell c + dI (+ the pair offsets)
+    for (unsigned long long rel = first; rel - 2u * lane < c_end; rel += STEP) {   // wave-uniform trip count
+        const unsigned long long c = base + rel;
+        const bool v0 = rel < c_end && c < P.n, v1 = rel + 1 < c_end && c + 1 < P.n;
+        sp_u32x4 O = {0u, 0u, 0u, 0u}, Jp = O, Kp = O, JK = O;
+        // the four pairs [x, x + 1] for x = c, c + dJ, c + dK, c + dJ + dK inside [0, n + SP_PAD)
+        if ((long long)c + dlo >= 0 && (long long)c + 1 + dhi <= (long long)(P.n + SP_PAD - 1)) {
+            const uint32_t boff = (uint32_t)c << 3;   // c < 2^29
+            (void)SDF_CHK(20, c, 0, P.n + SP_PAD);
+            O = *(const sp_u32x4 *)(bS + boff);
+            Jp = *(const sp_u32x4 *)(bJ + boff);
+            Kp = *(const sp_u32x4 *)(bK + boff);
+            JK = *(const sp_u32x4 *)(bJK + boff);
+        } else {   // the grid's edge: word by word, out-of-grid words 0 (no cell of the sweep's range reads them)
+            auto ld = [&](long long x) -> unsigned long long {
+                return (x >= 0 && x < (long long)P.n) ? P.S[SDF_CHK(22, x, 0, P.n)] : 0ull;
+            };
+            auto pair = [&](long long x) {
+                const unsigned long long a = ld(x), b = ld(x + 1);
+                return sp_u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+            };
+            const long long cc = (long long)c;
+            O = pair(cc);
+            Jp = pair(cc + dJ);
+            Kp = pair(cc + dK);
+            JK = pair(cc + dJ + dK);
+        }
+        // the i-upwind words of the pair's other cell: the neighbouring lane's pair elements (DPP), the
+        // wave's edge lane fetching its own
+        uint32_t e0 = 0u, e1 = 0u, e2 = 0u, e3 = 0u;   // O, J, K, JK words of cell c + dI (edge lane only)
+        if (lane == (pos ? 0u : 63u)) {
+            const long long x = (long long)c + dI;
+            auto ld1 = [&](long long y) -> uint32_t {
+                return (y >= 0 && y < (long long)P.n) ? (uint32_t)P.S[SDF_CHK(22, y, 0, P.n)] : 0u;
+            };
+            e0 = ld1(x);
+            e1 = ld1(x + dJ);
+            e2 = ld1(x + dK);
+            e3 = ld1(x + dJ + dK);
+        }
+        uint32_t t0, t1, t2, t3;   // cell c - 1's words (di > 0) or cell c + 2's (di < 0)
+        if (pos) {   // wave_shr:1 -- lane L takes lane L - 1's second cell; lane 0 keeps its own fetch
+            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O.z, 0x138, 0xf, 0xf, false);
+            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp.z, 0x138, 0xf, 0xf, false);
+            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp.z, 0x138, 0xf, 0xf, false);
+            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK.z, 0x138, 0xf, 0xf, false);
+        } else {     // wave_shl:1 -- lane L takes lane L + 1's first cell; lane 63 keeps its own fetch
+            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O.x, 0x130, 0xf, 0xf, false);
+            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp.x, 0x130, 0xf, 0xf, false);
+            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp.x, 0x130, 0xf, 0xf, false);
+            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK.x, 0x130, 0xf, 0xf, false);
+        }
+        // cell c + 1's coordinates
+        int i1 = i + 1, j1 = j, k1 = k;
+        if (i1 == P.ni) {
+            i1 = 0;
+            if (++j1 == P.nj) { j1 = 0; ++k1; }
+        }
+        unsigned f0 = 0u, f1 = 0u;
+        if (v0 && sp_in(P, i, j, k)) {   // q: i, j, ij, k, ik, jk, ijk (k_sp_jacobi's off[])
+            const uint32_t w[7] = {pos ? t0 : O.z, Jp.x, pos ? t1 : Jp.z, Kp.x, pos ? t2 : Kp.z, JK.x, pos ? t3 : JK.z};
+            const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
+            f0 = sp_any_scan(P, O.x, w, interior) ? 1u : 0u;
+        }
+        if (v1 && sp_in(P, i1, j1, k1)) {
+            const uint32_t w[7] = {pos ? O.x : t0, Jp.z, pos ? Jp.x : t1, Kp.z, pos ? Kp.x : t2, JK.z, pos ? JK.x : t3};
+            const bool interior = i1 >= 1 && i1 <= P.ni - 2 && j1 >= 1 && j1 <= P.nj - 2 && k1 >= 1 && k1 <= P.nk - 2;
+            f1 = sp_any_scan(P, O.z, w, interior) ? 1u : 0u;
+        }
+        if (!P.sv) {   // two buffers: the cells that keep their value are copied (in place they already hold it)
+            if (v0 && !f0) P.X[c] = ((unsigned long long)O.y << 32) | O.x;
+            if (v1 && !f1) P.X[c + 1] = ((unsigned long long)O.w << 32) | O.z;
+        }
+        // the list in address order: lane L's cells after those of lanes < L
+        const unsigned long long b0 = __ballot(f0 != 0u), b1 = __ballot(f1 != 0u), lt = (1ull << lane) - 1ull;
+        const unsigned at = cnt + (unsigned)(__builtin_popcountll(b0 & lt) + __builtin_popcountll(b1 & lt));
+        if (f0) buf[at] = (unsigned)c;
+        if (f1) buf[at + f0] = (unsigned)(c + 1);
+        cnt += (unsigned)(__builtin_popcountll(b0) + __builtin_popcountll(b1));
+        if (cnt > SP_JWAVE - 128) {
             sp_jlist_flush(P, part, buf, cnt, lane);
             cnt = 0;
         }
@@ -1731,8 +1879,12 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
 inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const SpParams &P)
 {
     if (SP_JSCAN_FAST && P.c_lo == 0 && P.n == (unsigned long long)P.ni * P.nj * P.nk && P.k_lo == 0 && P.k_hi == P.nk &&
-        P.n <= (1ull << 29) && blocks % 8 == 0)
-        hipLaunchKernelGGL((k_sp_jacobi<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+        P.n <= (1ull << 29) && blocks % 8 == 0) {
+        if (SP_JSCAN_PAIR && !getenv("SDFGEN_JSCAN_NARROW"))   // (diagnostics: SDFGEN_JSCAN_NARROW=1, the 8-load scan)
+            hipLaunchKernelGGL(k_sp_jscan2, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        else
+            hipLaunchKernelGGL((k_sp_jacobi<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+    }
     else
         hipLaunchKernelGGL((k_sp_jacobi<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
 }
@@ -1745,7 +1897,8 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
 {
     const unsigned long long n = (unsigned long long)ni * nj * nk;
     const int nw = (W.workers > 0 && W.workers <= SP_WORKERS) ? W.workers : SP_WORKERS;
-    if (int rc_ = sp_grow(&W.alt, &W.cap_alt, n, false, st)) return rc_;
+    // (the two state buffers swap: both carry k_sp_jscan2's padding)
+    if (int rc_ = sp_grow(&W.alt, &W.cap_alt, sp_pad(n), false, st)) return rc_;
     SpParams P;
     unsigned long long blocks = 0;
     if (int rc = sp_setup(W, st, soup, origin, dx, ni, nj, nk, sweep, 0, n, P, blocks)) return rc;
