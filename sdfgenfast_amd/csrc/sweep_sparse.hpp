@@ -146,8 +146,9 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                           // only "any candidate" (sp_any_scan) -- the scan is VALU-issue-bound since SP_VMASK
 #endif
 #ifndef SP_JSCAN_PAIR
-#define SP_JSCAN_PAIR 1   // the fast scan as k_sp_jscan2: two cells per lane, 16-byte loads (needs 2 cells of padding
-                          // past the grid in both state buffers: sp_pad)
+#define SP_JSCAN_PAIR 1   // the fast scan as k_sp_jscan2<NP>: 2 NP cells per lane, 16-byte loads (needs SP_PAD cells of
+                          // padding past the grid in both state buffers: sp_pad); 0 = the 8-load k_sp_jacobi<false, true>;
+                          // SDFGEN_JSCAN_NP (diagnostics) overrides: 0, 1, 2
 #endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
@@ -825,11 +826,13 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 // in the grid).  Same traversal (XCD eighths, one contiguous chunk per block), same list order (cells in
 // address order), same decision (sp_any_scan): the list equals k_sp_jacobi<false, true>'s.
 typedef uint32_t sp_u32x4 __attribute__((ext_vector_type(4), aligned(8)));   // two 8-byte cells, 8-byte aligned
-constexpr unsigned long long SP_PAD = 2;   // cells of padding past n in the state buffers (sp_pad)
+constexpr unsigned long long SP_PAD = 4;   // cells of padding past n in the state buffers (sp_pad)
 inline unsigned long long sp_pad(unsigned long long n) { return n + SP_PAD; }
 
-__global__ void __launch_bounds__(256) k_sp_jscan2(SpParams P)
+template <int NP>   // pairs per lane: 2 * NP consecutive cells, 4 * NP 16-byte loads issued together
+__global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan2(SpParams P)
 {
+    static_assert(NP >= 1 && 2 * NP <= SP_PAD + 1, "the last pair may read 2 NP - 1 cells past the grid");
     __shared__ unsigned s_list[4][SP_JWAVE];
     const unsigned lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD
@@ -841,9 +844,9 @@ __global__ void __launch_bounds__(256) k_sp_jscan2(SpParams P)
     const unsigned long long chunk = (span + nb * blockDim.x - 1) / (nb * blockDim.x) * blockDim.x;
     const unsigned long long c_beg = (unsigned long long)(blockIdx.x / 8) * chunk;
     const unsigned long long c_end = std::min(span, c_beg + chunk);
-    // an iteration covers 512 cells of the chunk: wave wv the 128 from wv * 128, lane L two of them
-    const unsigned long long first = c_beg + wv * 128u + 2u * lane;
-    constexpr unsigned STEP = 512;
+    // an iteration covers 512 NP cells of the chunk: wave wv the 128 NP from wv * 128 NP, lane L 2 NP of them
+    constexpr unsigned CL = 2 * NP, STEP = 512 * NP;
+    const unsigned long long first = c_beg + wv * (128u * NP) + CL * lane;
     int i, j, k, si, sj, sk;
     {
         const unsigned c0 = (unsigned)(base + first), r0 = c0 / (unsigned)P.ni;
@@ -860,19 +863,21 @@ __global__ void __launch_bounds__(256) k_sp_jscan2(SpParams P)
     const char *bS = (const char *)P.S, *bJ = (const char *)(P.S + dJ), *bK = (const char *)(P.S + dK),
                *bJK = (const char *)(P.S + dJ + dK);   // (scalar bases; a base may lie outside the buffer)
     const bool pos = P.di > 0;
-    const long long dI = pos ? -1 : 2;   // the edge lane's own fetch: cell c + dI (+ the pair offsets)
-    for (unsigned long long rel = first; rel - 2u * lane < c_end; rel += STEP) {   // wave-uniform trip count
+    const long long dI = pos ? -1 : CL;   // the edge lane's own fetch: cell c + dI (+ the pair offsets)
+    for (unsigned long long rel = first; rel - CL * lane < c_end; rel += STEP) {   // wave-uniform trip count
         const unsigned long long c = base + rel;
-        const bool v0 = rel < c_end && c < P.n, v1 = rel + 1 < c_end && c + 1 < P.n;
-        sp_u32x4 O = {0u, 0u, 0u, 0u}, Jp = O, Kp = O, JK = O;
-        // the four pairs [x, x + 1] for x = c, c + dJ, c + dK, c + dJ + dK inside [0, n + SP_PAD)
-        if ((long long)c + dlo >= 0 && (long long)c + 1 + dhi <= (long long)(P.n + SP_PAD - 1)) {
+        sp_u32x4 O[NP], Jp[NP], Kp[NP], JK[NP];
+        // every pair [x, x + 1] for x = c + 2p + {0, dJ, dK, dJ + dK} inside [0, n + SP_PAD)
+        if ((long long)c + dlo >= 0 && (long long)c + CL - 1 + dhi <= (long long)(P.n + SP_PAD - 1)) {
             const uint32_t boff = (uint32_t)c << 3;   // c < 2^29
             (void)SDF_CHK(20, c, 0, P.n + SP_PAD);
-            O = *(const sp_u32x4 *)(bS + boff);
-            Jp = *(const sp_u32x4 *)(bJ + boff);
-            Kp = *(const sp_u32x4 *)(bK + boff);
-            JK = *(const sp_u32x4 *)(bJK + boff);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                O[p] = *(const sp_u32x4 *)(bS + boff + 16 * p);
+                Jp[p] = *(const sp_u32x4 *)(bJ + boff + 16 * p);
+                Kp[p] = *(const sp_u32x4 *)(bK + boff + 16 * p);
+                JK[p] = *(const sp_u32x4 *)(bJK + boff + 16 * p);
+            }
         } else {   // the grid's edge: word by word, out-of-grid words 0 (no cell of the sweep's range reads them)
             auto ld = [&](long long x) -> unsigned long long {
                 return (x >= 0 && x < (long long)P.n) ? P.S[SDF_CHK(22, x, 0, P.n)] : 0ull;
@@ -881,15 +886,18 @@ __global__ void __launch_bounds__(256) k_sp_jscan2(SpParams P)
                 const unsigned long long a = ld(x), b = ld(x + 1);
                 return sp_u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
             };
-            const long long cc = (long long)c;
-            O = pair(cc);
-            Jp = pair(cc + dJ);
-            Kp = pair(cc + dK);
-            JK = pair(cc + dJ + dK);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const long long cc = (long long)c + 2 * p;
+                O[p] = pair(cc);
+                Jp[p] = pair(cc + dJ);
+                Kp[p] = pair(cc + dK);
+                JK[p] = pair(cc + dJ + dK);
+            }
         }
-        // the i-upwind words of the pair's other cell: the neighbouring lane's pair elements (DPP), the
-        // wave's edge lane fetching its own
-        uint32_t e0 = 0u, e1 = 0u, e2 = 0u, e3 = 0u;   // O, J, K, JK words of cell c + dI (edge lane only)
+        // the i-upwind words of the lane's first cell (di > 0: cell c - 1) or last (di < 0: cell c + 2 NP) come
+        // from the neighbouring lane by DPP; the wave's edge lane fetches its own
+        uint32_t e0 = 0u, e1 = 0u, e2 = 0u, e3 = 0u;
         if (lane == (pos ? 0u : 63u)) {
             const long long x = (long long)c + dI;
             auto ld1 = [&](long long y) -> uint32_t {
@@ -900,46 +908,67 @@ __global__ void __launch_bounds__(256) k_sp_jscan2(SpParams P)
             e2 = ld1(x + dK);
             e3 = ld1(x + dJ + dK);
         }
-        uint32_t t0, t1, t2, t3;   // cell c - 1's words (di > 0) or cell c + 2's (di < 0)
-        if (pos) {   // wave_shr:1 -- lane L takes lane L - 1's second cell; lane 0 keeps its own fetch
-            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O.z, 0x138, 0xf, 0xf, false);
-            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp.z, 0x138, 0xf, 0xf, false);
-            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp.z, 0x138, 0xf, 0xf, false);
-            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK.z, 0x138, 0xf, 0xf, false);
+        uint32_t t0, t1, t2, t3;
+        if (pos) {   // wave_shr:1 -- lane L takes lane L - 1's last cell; lane 0 keeps its own fetch
+            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O[NP - 1].z, 0x138, 0xf, 0xf, false);
+            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp[NP - 1].z, 0x138, 0xf, 0xf, false);
+            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp[NP - 1].z, 0x138, 0xf, 0xf, false);
+            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK[NP - 1].z, 0x138, 0xf, 0xf, false);
         } else {     // wave_shl:1 -- lane L takes lane L + 1's first cell; lane 63 keeps its own fetch
-            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O.x, 0x130, 0xf, 0xf, false);
-            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp.x, 0x130, 0xf, 0xf, false);
-            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp.x, 0x130, 0xf, 0xf, false);
-            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK.x, 0x130, 0xf, 0xf, false);
+            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O[0].x, 0x130, 0xf, 0xf, false);
+            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp[0].x, 0x130, 0xf, 0xf, false);
+            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp[0].x, 0x130, 0xf, 0xf, false);
+            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK[0].x, 0x130, 0xf, 0xf, false);
         }
-        // cell c + 1's coordinates
-        int i1 = i + 1, j1 = j, k1 = k;
-        if (i1 == P.ni) {
-            i1 = 0;
-            if (++j1 == P.nj) { j1 = 0; ++k1; }
-        }
-        unsigned f0 = 0u, f1 = 0u;
-        if (v0 && sp_in(P, i, j, k)) {   // q: i, j, ij, k, ik, jk, ijk (k_sp_jacobi's off[])
-            const uint32_t w[7] = {pos ? t0 : O.z, Jp.x, pos ? t1 : Jp.z, Kp.x, pos ? t2 : Kp.z, JK.x, pos ? t3 : JK.z};
-            const bool interior = i >= 1 && i <= P.ni - 2 && j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
-            f0 = sp_any_scan(P, O.x, w, interior) ? 1u : 0u;
-        }
-        if (v1 && sp_in(P, i1, j1, k1)) {
-            const uint32_t w[7] = {pos ? O.x : t0, Jp.z, pos ? Jp.x : t1, Kp.z, pos ? Kp.x : t2, JK.z, pos ? JK.x : t3};
-            const bool interior = i1 >= 1 && i1 <= P.ni - 2 && j1 >= 1 && j1 <= P.nj - 2 && k1 >= 1 && k1 <= P.nk - 2;
-            f1 = sp_any_scan(P, O.z, w, interior) ? 1u : 0u;
-        }
-        if (!P.sv) {   // two buffers: the cells that keep their value are copied (in place they already hold it)
-            if (v0 && !f0) P.X[c] = ((unsigned long long)O.y << 32) | O.x;
-            if (v1 && !f1) P.X[c + 1] = ((unsigned long long)O.w << 32) | O.z;
+        unsigned f[CL];
+        int ic = i, jc = j, kc = k;   // coordinates of cell c + m, advanced along the row
+#pragma unroll
+        for (int m = 0; m < CL; ++m) {
+            const int p = m >> 1;
+            const bool hi = m & 1;
+            // this cell's words and its i-upwind cell's (q: i, j, ij, k, ik, jk, ijk; k_sp_jacobi's off[])
+            const uint32_t wo = hi ? O[p].z : O[p].x, wj = hi ? Jp[p].z : Jp[p].x, wk = hi ? Kp[p].z : Kp[p].x,
+                           wjk = hi ? JK[p].z : JK[p].x;
+            uint32_t ui, uj, uk, ujk;   // the i-upwind cell's words
+            if (pos) {
+                if (m == 0) { ui = t0; uj = t1; uk = t2; ujk = t3; }
+                else if (hi) { ui = O[p].x; uj = Jp[p].x; uk = Kp[p].x; ujk = JK[p].x; }
+                else { ui = O[p - 1].z; uj = Jp[p - 1].z; uk = Kp[p - 1].z; ujk = JK[p - 1].z; }
+            } else {
+                if (m == CL - 1) { ui = t0; uj = t1; uk = t2; ujk = t3; }
+                else if (!hi) { ui = O[p].z; uj = Jp[p].z; uk = Kp[p].z; ujk = JK[p].z; }
+                else { ui = O[p + 1].x; uj = Jp[p + 1].x; uk = Kp[p + 1].x; ujk = JK[p + 1].x; }
+            }
+            const bool v = rel + m < c_end && c + m < P.n;
+            f[m] = 0u;
+            if (v && sp_in(P, ic, jc, kc)) {
+                const uint32_t w[7] = {ui, wj, uj, wk, uk, wjk, ujk};
+                const bool interior = ic >= 1 && ic <= P.ni - 2 && jc >= 1 && jc <= P.nj - 2 && kc >= 1 && kc <= P.nk - 2;
+                f[m] = sp_any_scan(P, wo, w, interior) ? 1u : 0u;
+            }
+            if (!P.sv && v && !f[m])   // two buffers: cells that keep their value are copied (in place they hold it)
+                P.X[c + m] = ((unsigned long long)(hi ? O[p].w : O[p].y) << 32) | wo;
+            if (++ic == P.ni) {
+                ic = 0;
+                if (++jc == P.nj) { jc = 0; ++kc; }
+            }
         }
         // the list in address order: lane L's cells after those of lanes < L
-        const unsigned long long b0 = __ballot(f0 != 0u), b1 = __ballot(f1 != 0u), lt = (1ull << lane) - 1ull;
-        const unsigned at = cnt + (unsigned)(__builtin_popcountll(b0 & lt) + __builtin_popcountll(b1 & lt));
-        if (f0) buf[at] = (unsigned)c;
-        if (f1) buf[at + f0] = (unsigned)(c + 1);
-        cnt += (unsigned)(__builtin_popcountll(b0) + __builtin_popcountll(b1));
-        if (cnt > SP_JWAVE - 128) {
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        unsigned at = cnt, tot = 0;
+#pragma unroll
+        for (int m = 0; m < CL; ++m) {
+            const unsigned long long bm = __ballot(f[m] != 0u);
+            at += (unsigned)__builtin_popcountll(bm & lt);
+            tot += (unsigned)__builtin_popcountll(bm);
+        }
+#pragma unroll
+        for (int m = 0; m < CL; ++m) {
+            if (f[m]) buf[at] = (unsigned)(c + m);
+            at += f[m];
+        }
+        cnt += tot;
+        if (cnt > SP_JWAVE - 64 * CL) {
             sp_jlist_flush(P, part, buf, cnt, lane);
             cnt = 0;
         }
@@ -1880,8 +1909,9 @@ inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const Sp
 {
     if (SP_JSCAN_FAST && P.c_lo == 0 && P.n == (unsigned long long)P.ni * P.nj * P.nk && P.k_lo == 0 && P.k_hi == P.nk &&
         P.n <= (1ull << 29) && blocks % 8 == 0) {
-        if (SP_JSCAN_PAIR && !getenv("SDFGEN_JSCAN_NARROW"))   // (diagnostics: SDFGEN_JSCAN_NARROW=1, the 8-load scan)
-            hipLaunchKernelGGL(k_sp_jscan2, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        static const int np = getenv("SDFGEN_JSCAN_NP") ? atoi(getenv("SDFGEN_JSCAN_NP")) : SP_JSCAN_PAIR;
+        if (np == 2) hipLaunchKernelGGL(k_sp_jscan2<2>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        else if (np == 1) hipLaunchKernelGGL(k_sp_jscan2<1>, dim3((unsigned)blocks), dim3(256), 0, st, P);
         else
             hipLaunchKernelGGL((k_sp_jacobi<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
     }

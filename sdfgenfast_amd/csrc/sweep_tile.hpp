@@ -1514,13 +1514,21 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
 // (the role tests are conditional operators on ROLE, a constant with one helper wave: clang emits only the
 // live arm, so the one-helper code is the original's instruction for instruction)
+// ST_MASKED (A/B): the gathers and stage-1 loads only in the lanes that use them (exec-masked) instead of
+// every lane reading a dummy: a wave-wide load costs the texture addresser per lane
+#ifndef ST_MASKED
+#define ST_MASKED 0
+#endif
 #define ST_GATHER(g, cg, qg)                                                                          \
-    const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
-    const float4 oa##g = ROLE != 2 ? P.soup[so##g] : z4, ob##g = ROLE != 2 ? P.soup[so##g + 1] : z4,    \
-                 oc##g = ROLE != 2 ? P.soup[so##g + 2] : z4;                                           \
-    const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
-    const float4 ha##g = ROLE != 1 ? P.soup[sh##g] : z4, hb##g = ROLE != 1 ? P.soup[sh##g + 1] : z4,    \
-                 hc##g = ROLE != 1 ? P.soup[sh##g + 2] : z4;
+    const bool go##g = ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0, gh##g = (g) < hp && lbl_of((uint32_t)(qg)) >= 0; \
+    const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && go##g ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
+    const float4 oa##g = (ROLE != 2 && (!ST_MASKED || go##g)) ? P.soup[so##g] : z4,                     \
+                 ob##g = (ROLE != 2 && (!ST_MASKED || go##g)) ? P.soup[so##g + 1] : z4,                 \
+                 oc##g = (ROLE != 2 && (!ST_MASKED || go##g)) ? P.soup[so##g + 2] : z4;                 \
+    const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && gh##g ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
+    const float4 ha##g = (ROLE != 1 && (!ST_MASKED || gh##g)) ? P.soup[sh##g] : z4,                     \
+                 hb##g = (ROLE != 1 && (!ST_MASKED || gh##g)) ? P.soup[sh##g + 1] : z4,                 \
+                 hc##g = (ROLE != 1 && (!ST_MASKED || gh##g)) ? P.soup[sh##g + 2] : z4;
                 ST_GATHER(0, c0, q0)
                 ST_GATHER(1, c1, q1)
 #if ST_G_DEF > 2
@@ -1542,11 +1550,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
         const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
-        cn = ROLE != 2 ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;                               \
+        cn = (ROLE != 2 && (!ST_MASKED || ok_)) ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;      \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
                        : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + hB + (g)); \
-        qn = ROLE != 1 ? __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE) : 0ull;                      \
+        qn = (ROLE != 1 && (!ST_MASKED || (g) < hcB)) ? __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE) : 0ull; \
     }
                 // Always issued (a fixed count keeps the waits below precise); slots with nothing
                 // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
