@@ -1519,16 +1519,24 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #ifndef ST_MASKED
 #define ST_MASKED 0
 #endif
+#if ST_MASKED
 #define ST_GATHER(g, cg, qg)                                                                          \
     const bool go##g = ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0, gh##g = (g) < hp && lbl_of((uint32_t)(qg)) >= 0; \
     const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && go##g ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
-    const float4 oa##g = (ROLE != 2 && (!ST_MASKED || go##g)) ? P.soup[so##g] : z4,                     \
-                 ob##g = (ROLE != 2 && (!ST_MASKED || go##g)) ? P.soup[so##g + 1] : z4,                 \
-                 oc##g = (ROLE != 2 && (!ST_MASKED || go##g)) ? P.soup[so##g + 2] : z4;                 \
+    const float4 oa##g = (ROLE != 2 && go##g) ? P.soup[so##g] : z4, ob##g = (ROLE != 2 && go##g) ? P.soup[so##g + 1] : z4, \
+                 oc##g = (ROLE != 2 && go##g) ? P.soup[so##g + 2] : z4;                                \
     const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && gh##g ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
-    const float4 ha##g = (ROLE != 1 && (!ST_MASKED || gh##g)) ? P.soup[sh##g] : z4,                     \
-                 hb##g = (ROLE != 1 && (!ST_MASKED || gh##g)) ? P.soup[sh##g + 1] : z4,                 \
-                 hc##g = (ROLE != 1 && (!ST_MASKED || gh##g)) ? P.soup[sh##g + 2] : z4;
+    const float4 ha##g = (ROLE != 1 && gh##g) ? P.soup[sh##g] : z4, hb##g = (ROLE != 1 && gh##g) ? P.soup[sh##g + 1] : z4, \
+                 hc##g = (ROLE != 1 && gh##g) ? P.soup[sh##g + 2] : z4;
+#else
+#define ST_GATHER(g, cg, qg)                                                                          \
+    const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
+    const float4 oa##g = ROLE != 2 ? P.soup[so##g] : z4, ob##g = ROLE != 2 ? P.soup[so##g + 1] : z4,    \
+                 oc##g = ROLE != 2 ? P.soup[so##g + 2] : z4;                                           \
+    const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
+    const float4 ha##g = ROLE != 1 ? P.soup[sh##g] : z4, hb##g = ROLE != 1 ? P.soup[sh##g + 1] : z4,    \
+                 hc##g = ROLE != 1 ? P.soup[sh##g + 2] : z4;
+#endif
                 ST_GATHER(0, c0, q0)
                 ST_GATHER(1, c1, q1)
 #if ST_G_DEF > 2
@@ -1550,7 +1558,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         const int a_ = fB + (g) - bl - cl;                                                             \
         const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
         const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
-        cn = (ROLE != 2 && (!ST_MASKED || ok_)) ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;      \
+        cn = (ROLE != 2 && (!ST_MASKED || ok_)) ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;       \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
                        : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + hB + (g)); \
