@@ -863,7 +863,7 @@ __global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan2(SpParams P)
     const char *bS = (const char *)P.S, *bJ = (const char *)(P.S + dJ), *bK = (const char *)(P.S + dK),
                *bJK = (const char *)(P.S + dJ + dK);   // (scalar bases; a base may lie outside the buffer)
     const bool pos = P.di > 0;
-    const long long dI = pos ? -1 : CL;   // the edge lane's own fetch: cell c + dI (+ the pair offsets)
+    const long long dI = pos ? -1ll : (long long)CL;   // (both signed: -1 : CL would be unsigned) the edge lane's own fetch: cell c + dI (+ the pair offsets)
     for (unsigned long long rel = first; rel - CL * lane < c_end; rel += STEP) {   // wave-uniform trip count
         const unsigned long long c = base + rel;
         sp_u32x4 O[NP], Jp[NP], Kp[NP], JK[NP];
