@@ -209,6 +209,8 @@ struct SpParams {
     int tm_m;                          // second-pass sweep index 0..7 for tm
 };
 
+typedef uint32_t sp_u32x4 __attribute__((ext_vector_type(4), aligned(8)));   // two 8-byte cells, 8-byte aligned
+
 __device__ __forceinline__ unsigned long long sp_ld64(const unsigned long long *p)
 {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -667,14 +669,34 @@ __device__ __forceinline__ void sp_push(const SpParams &P, int i, int j, int k, 
 // labels.  This relies on the 8-byte cell stores never tearing (one global_store_dwordx2 per cell)
 // and on S / X never being declared __restrict__ or read through the constant cache: the compiler must
 // not assume the stores leave S unchanged.
-template <bool SLAB = false>
+// PAIR (one device): the cell and its 7 upwind low words from four 16-byte loads instead of eight narrow ones
+// (the list pass ran at 56 % TA busy at C4, profiles/r06_limiter_c4.json): the pairs (c - 1, c) for di > 0 or
+// (c, c + 1) for di < 0, at the cell and at its j-, k- and jk-upwind cells -- all inside the grid for a
+// listed cell (it lies in the sweep's range, so every upwind neighbour exists).
+template <bool SLAB = false, bool PAIR = false>
 __device__ __forceinline__ void sp_jacobi_cell(const SpParams &P, unsigned c32, unsigned *qmask, size_t (&tgt)[7])
 {
     const int i = (int)(c32 % (unsigned)P.ni);
     const unsigned r = c32 / (unsigned)P.ni;
     const int j = (int)(r % (unsigned)P.nj), k = (int)(r / (unsigned)P.nj);
-    const unsigned long long s = P.S[SDF_CHK(20, c32, P.c_lo, P.c_lo + P.n)];
-    const unsigned long long y = sp_eval<false, SLAB>(P, P.S, i, j, k, c32, s);
+    unsigned long long s, y;
+    if constexpr (PAIR && !SLAB) {
+        const long long dJ = -(long long)P.dj * P.ni, dK = -(long long)P.dk * P.ni * P.nj;
+        const bool pos = P.di > 0;
+        const unsigned long long *b = P.S + (long long)c32 - (pos ? 1 : 0);   // the pair holding the cell
+        (void)SDF_CHK(22, (unsigned long long)((long long)c32 - (pos ? 1 : 0) + std::min(dJ, 0ll) + std::min(dK, 0ll)), 0, P.n);
+        (void)SDF_CHK(22, (unsigned long long)((long long)c32 + (pos ? 0 : 1) + std::max(dJ, 0ll) + std::max(dK, 0ll)), 0, P.n);
+        const sp_u32x4 O = *(const sp_u32x4 *)b, Jp = *(const sp_u32x4 *)(b + dJ), Kp = *(const sp_u32x4 *)(b + dK),
+                       JK = *(const sp_u32x4 *)(b + dJ + dK);
+        // the cell is element 1 of its pairs for di > 0 (element 0 its i-upwind neighbour), element 0 for di < 0
+        s = pos ? (((unsigned long long)O.w << 32) | O.z) : (((unsigned long long)O.y << 32) | O.x);
+        const uint32_t w[7] = {pos ? O.x : O.z, pos ? Jp.z : Jp.x, pos ? Jp.x : Jp.z, pos ? Kp.z : Kp.x,
+                               pos ? Kp.x : Kp.z, pos ? JK.z : JK.x, pos ? JK.x : JK.z};
+        y = sp_eval_w<false>(P, i, j, k, s, w);
+    } else {
+        s = P.S[SDF_CHK(20, c32, P.c_lo, P.c_lo + P.n)];
+        y = sp_eval<false, SLAB>(P, P.S, i, j, k, c32, s);
+    }
     if (!P.sv) {
         P.X[SDF_CHK(21, c32, P.c_lo, P.c_lo + P.n)] = y;
     } else if (y != s) {   // in place: keep the pre-sweep value, then change the cell
@@ -825,7 +847,6 @@ __global__ void __launch_bounds__(256) k_sp_jacobi(SpParams P)
 // sources are right for every cell that needs them (a cell of the sweep's range has all its upwind words
 // in the grid).  Same traversal (XCD eighths, one contiguous chunk per block), same list order (cells in
 // address order), same decision (sp_any_scan): the list equals k_sp_jacobi<false, true>'s.
-typedef uint32_t sp_u32x4 __attribute__((ext_vector_type(4), aligned(8)));   // two 8-byte cells, 8-byte aligned
 constexpr unsigned long long SP_PAD = 4;   // cells of padding past n in the state buffers (sp_pad)
 inline unsigned long long sp_pad(unsigned long long n) { return n + SP_PAD; }
 
@@ -986,7 +1007,7 @@ __global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan2(SpParams P)
 // Pass 1b: the listed cells, each exactly as in place (sp_eval against S).
 // Z-slab: it pushes into the neighbours' live halos, so it runs after k_sp_slab_wait saw both
 // neighbours READY.
-template <bool SLAB>
+template <bool SLAB, bool PAIR = false>
 __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
 {
     const unsigned part = blockIdx.x % SP_JPARTS;
@@ -999,7 +1020,7 @@ __global__ void __launch_bounds__(256) k_sp_jlist(SpParams P)
          x += (unsigned long long)(gridDim.x / SP_JPARTS) * blockDim.x) {
         unsigned qmask = 0;
         size_t tgt[7];
-        if (x < cnt) sp_jacobi_cell<SLAB>(P, list[x], &qmask, tgt);
+        if (x < cnt) sp_jacobi_cell<SLAB, PAIR>(P, list[x], &qmask, tgt);
         sp_append_wave(P, (unsigned)(((blockIdx.x * blockDim.x + threadIdx.x) >> 6) & (P.nq - 1u)), qmask, tgt, false);
     }
 }
@@ -1919,6 +1940,18 @@ inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const Sp
         hipLaunchKernelGGL((k_sp_jacobi<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
 }
 
+// The one-device list pass: its cells' words by 16-byte pair loads (SP_JLIST_PAIR; SDFGEN_JLIST_NARROW=1,
+// diagnostics: the eight narrow loads)
+#ifndef SP_JLIST_PAIR
+#define SP_JLIST_PAIR 1
+#endif
+inline void sp_launch_jlist(unsigned long long blocks, hipStream_t st, const SpParams &P)
+{
+    static const bool narrow = !SP_JLIST_PAIR || getenv("SDFGEN_JLIST_NARROW") != nullptr;
+    if (narrow) hipLaunchKernelGGL((k_sp_jlist<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+    else hipLaunchKernelGGL((k_sp_jlist<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
+}
+
 // Enqueue one sparse sweep on `st`: reads *cell, writes the other buffer, then swaps
 // the two so *cell holds the result.  Returns 0 or a negative SDFGEN_HIP_E* code.
 inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup, unsigned long long **cell,
@@ -1957,7 +1990,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         P.sv = W.alt;
         sp_launch_jacobi(blocks, st, P);
         if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
-        hipLaunchKernelGGL(k_sp_jlist<false>, dim3(SP_JLIST_PER_PART * SP_JPARTS), dim3(256), 0, st, P);
+        sp_launch_jlist(SP_JLIST_PER_PART * SP_JPARTS, st, P);
         if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
         if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
@@ -1968,7 +2001,7 @@ inline int sparse_sweep(SparseSweepWorkspace &W, hipStream_t st, const float4 *s
         sp_launch_jacobi(blocks, st, P);
         if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         const unsigned long long lblocks = SP_JLIST_PER_PART * SP_JPARTS;   // k_sp_jlist: part = blockIdx % SP_JPARTS
-        hipLaunchKernelGGL(k_sp_jlist<false>, dim3((unsigned)lblocks), dim3(256), 0, st, P);
+        sp_launch_jlist(lblocks, st, P);
         if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
         hipLaunchKernelGGL(k_sp_recheck<false>, dim3(nw), dim3(64), 0, st, P);
         if (hipError_t e_ = hipGetLastError(); e_ != hipSuccess) return sdf_hip_rc(e_);
