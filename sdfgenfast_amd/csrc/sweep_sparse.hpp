@@ -146,9 +146,11 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                           // only "any candidate" (sp_any_scan) -- the scan is VALU-issue-bound since SP_VMASK
 #endif
 #ifndef SP_JSCAN_PAIR
-#define SP_JSCAN_PAIR 1   // the fast scan as k_sp_jscan2<NP>: 2 NP cells per lane, 16-byte loads (needs SP_PAD cells of
+#define SP_JSCAN_PAIR 2   // the fast scan as k_sp_jscan2<NP>: 2 NP cells per lane, 16-byte loads (needs SP_PAD cells of
                           // padding past the grid in both state buffers: sp_pad); 0 = the 8-load k_sp_jacobi<false, true>;
-                          // SDFGEN_JSCAN_NP (diagnostics) overrides: 0, 1, 2
+                          // SDFGEN_JSCAN_NP (diagnostics) overrides: 0, 1, 2.  Second pass, interleaved A/B
+                          // (profiles/r06g_ab_jscan_c{3,4}.log): C4 11.05 (0) / 10.44 (1) / 10.43-10.46 ms (2),
+                          // C3 2.60 / 2.66 / 2.57-2.60 ms; scan launch C4 630 -> 518 us (2)
 #endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
@@ -1940,10 +1942,10 @@ inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const Sp
         hipLaunchKernelGGL((k_sp_jacobi<false, false>), dim3((unsigned)blocks), dim3(256), 0, st, P);
 }
 
-// The one-device list pass: its cells' words by 16-byte pair loads (SP_JLIST_PAIR; SDFGEN_JLIST_NARROW=1,
-// diagnostics: the eight narrow loads)
+// The one-device list pass: its cells' words by 16-byte pair loads (SP_JLIST_PAIR, A/B) or eight narrow loads
+// (SDFGEN_JLIST_NARROW=1 forces those)
 #ifndef SP_JLIST_PAIR
-#define SP_JLIST_PAIR 1
+#define SP_JLIST_PAIR 0   // measured neutral at C3 (38.2 vs 37.9 us) and slower at C4 (275 vs 264 us per sweep): off
 #endif
 inline void sp_launch_jlist(unsigned long long blocks, hipStream_t st, const SpParams &P)
 {
