@@ -2206,25 +2206,33 @@ int sdfgen_hip_release(void)
 {
     DeviceGuard dg_;
     std::lock_guard<std::mutex> lk(g_mu);
+    // every workspace is freed; the first failing call (a sticky fault of an earlier kernel surfaces here)
+    // is what the return code reports
+    hipError_t first = hipSuccess;
+    auto chk = [&first](hipError_t e) { if (first == hipSuccess && e != hipSuccess) first = e; };
     for (Workspace *w : g_ws) {
-        hipSetDevice(w->device);
-        hipFree(w->cell);
-        hipFree(w->cnt);
-        hipFree(w->soup);
-        hipFree(w->tri);
-        hipFree(w->xyz);
-        hipFree(w->err_flag);
-        hipFree(w->evals);
-        hipFree(w->status);
-        hipFree(w->out);
+        chk(hipSetDevice(w->device));
+        chk(hipFree(w->cell));
+        chk(hipFree(w->cnt));
+        chk(hipFree(w->soup));
+        chk(hipFree(w->tri));
+        chk(hipFree(w->xyz));
+        chk(hipFree(w->err_flag));
+        chk(hipFree(w->evals));
+        chk(hipFree(w->status));
+        chk(hipFree(w->out));
         tile_sweep_release(w->wf);
         sparse_sweep_release(w->sp);
         band_release(w->band);
-        for (auto &e : w->ev) hipEventDestroy(e);
-        hipStreamDestroy(w->stream);
+        for (auto &e : w->ev) chk(hipEventDestroy(e));
+        chk(hipStreamDestroy(w->stream));
         delete w;
     }
     g_ws.clear();
+    if (first != hipSuccess) {
+        sdf_last_hip = first;
+        return SDFGEN_HIP_ERUNTIME;
+    }
     // the pool of uncached communication blocks and the imported neighbour blocks (Z-slabs over IPC) are
     // kept: freeing them is what the pool avoids; sdfgen_hip_slab_close_imports is the
     // caller's explicit choice
@@ -2271,8 +2279,8 @@ int sdfgen_hip_debug_ptd(int device, int variant, uint64_t n, const float *pts, 
     hipLaunchKernelGGL(k_debug_ptd, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, dp, dout, variant);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(out, dout, n * sizeof(float), hipMemcpyDeviceToHost));
-    hipFree(dp);
-    hipFree(dout);
+    HIPCHK(hipFree(dp));
+    HIPCHK(hipFree(dout));
     return 0;
 }
 
@@ -2289,8 +2297,8 @@ int sdfgen_hip_debug_pit2d(int device, uint64_t n, const double *pit, double *ou
     hipLaunchKernelGGL(k_debug_pit2d, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, n, dp, dout);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpy(out4, dout, n * 4 * sizeof(double), hipMemcpyDeviceToHost));
-    hipFree(dp);
-    hipFree(dout);
+    HIPCHK(hipFree(dp));
+    HIPCHK(hipFree(dout));
     return 0;
 }
 

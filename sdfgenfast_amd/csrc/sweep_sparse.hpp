@@ -648,7 +648,7 @@ constexpr int SP_JWAVE = 256;   // LDS list entries per wave
 __device__ __forceinline__ void sp_push(const SpParams &P, int i, int j, int k, size_t c, uint32_t w)
 {
     const size_t hp = (size_t)i + (size_t)P.ni * j;
-    SDF_CHK(27, hp, 0, (size_t)P.ni * P.nj);
+    (void)SDF_CHK(27, hp, 0, (size_t)P.ni * P.nj);
     if (k == P.k_last && P.push_down_halo) {
         __hip_atomic_store(P.push_down_halo + hp, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

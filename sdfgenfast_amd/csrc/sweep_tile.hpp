@@ -66,6 +66,13 @@ namespace sdfhip {
 #ifndef ST_G_DEF
 #define ST_G_DEF 2     // helper batch: steps / halo entries per global round trip (2 or 4)
 #endif
+#ifndef ST_CWA
+#define ST_CWA 1       // helper: own cells' words loaded up to ST_RC steps ahead into LDS (their gathers then wait for a
+                       // free own slot only: one round trip from slot to landing instead of two)
+#endif
+#ifndef ST_RC_DEF
+#define ST_RC_DEF 8    // ST_CWA: own cell-word slots (power of two)
+#endif
 #ifndef ST_WORK_PRIO
 #define ST_WORK_PRIO 2   // compute waves' issue priority while stepping (0 while they wait)
 #endif
@@ -102,9 +109,11 @@ constexpr int ST_NSTREAM = 2 * ST_T + 1;      // halo streams: b-edge (8), c-edg
 constexpr int ST_RO = ST_RO_DEF;
 constexpr int ST_RH = ST_RH_DEF;
 constexpr int ST_G = ST_G_DEF;
+constexpr int ST_RC = ST_RC_DEF;
 typedef int i4v __attribute__((ext_vector_type(4)));
 static_assert((ST_RO & (ST_RO - 1)) == 0 && ST_RO >= ST_G, "own slots: power of two >= batch");
 static_assert((ST_RH & (ST_RH - 1)) == 0 && ST_RH >= 2 * ST_G, "halo slots: power of two");
+static_assert((ST_RC & (ST_RC - 1)) == 0 && ST_RC >= 2 * ST_G, "own cell-word slots: power of two >= 2 batches");
 
 // Tile kernel configuration: compute waves per tile, neighbour ring slots, twin lanes, the waves
 // per SIMD the register budget must allow, and lanes per cell (4: quad lanes, 2: duo lanes).
@@ -218,6 +227,20 @@ constexpr int ST_NSTATS = 24;                 // statistics words (StParams::sta
 
 // Entry layout in LDS: [3e] = (x1, w), [3e+1] = (x2, phi -- own entries only), [3e+2] = x3,
 // where w is the cell's low word (label and the sweep that set it: geom.hpp lo_word).
+
+// The lane id, recomputed where it is used (two VALU): a volatile asm is neither hoisted nor merged with another
+// copy, so a lane constant derived from it (an LDS entry base) is not held across the helper loop -- held, the
+// 128-VGPR quad kernel spilled it, and the landing's scratch reload (the youngest vector-memory op) turned the
+// wait for the gathers into a wait for every load in flight, the stage-1 polls included (ST_LANE_REMAT)
+#ifndef ST_LANE_REMAT
+#define ST_LANE_REMAT 1
+#endif
+__device__ __forceinline__ int st_lane_remat()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 
 // granule = {epoch (32 bits), low word (32 bits)}: the data is the flag
 __device__ __forceinline__ unsigned long long st_granule(unsigned epoch, uint32_t w)
@@ -418,6 +441,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     __shared__ int s_halo_ready[ST_NSTREAM + 1];
     __shared__ int s_abort;
     __shared__ int s_task;
+    // ST_CWA: own cells' words (phi, label) of steps [fA, fCl) for the helper's gathers, slot (step & (RC - 1))
+    __shared__ unsigned long long s_cw[ST_CWA ? ST_RC * ST_NCOL : 1];
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
@@ -1456,6 +1481,9 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             // (0 when the triangle count is unknown: ntri is ~0 until a pipeline sets it)
             const int gdum = (P.ntri >= 1 && P.ntri < 0x7fffffffull) ? (int)((unsigned)(J * 40503 + K * 9973 + 17) % (unsigned)P.ntri) : 0;
             int fA = ROLE == 2 ? nsteps : 0, gA = 0;   // own steps [fA, fA+gA) whose cells are in c0..c3 (ROLE 2: none)
+            // ST_CWA: the own steps' cell words run ahead of the gathers -- [fA, fCl) are in s_cw, [fCl, fCl + gCl)
+            // in flight in c0..c3; gA is then the batch gathered in this iteration
+            int fCl = fA, gCl = 0;
             int hA = hvalid ? 0 : P.A, hcA = 0;    // halo entries [hA, hA+hcA) whose granules are in q0..q3
             unsigned long long c0 = ~0ull, c1 = ~0ull, c2 = ~0ull, c3 = ~0ull;   // ST_G == 4 (named, never an array:
             unsigned long long q0 = 0, q1 = 0, q2 = 0, q3 = 0;                 //  arrays here landed in scratch)
@@ -1473,15 +1501,15 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #pragma unroll
                 for (int w = 1; w < ST_NCW; ++w) prog = min(prog, lds_ld(&s_hdr[1 + w]));
                 if (lds_ld(&s_abort)) break;
-                if (idle && gA == 0 && hcA == 0) {
+                if (idle && (ST_CWA ? gCl : gA) == 0 && hcA == 0) {
                     // Nothing in flight and the last round found nothing to do: wait cheaply (LDS
                     // progress, at most one granule probe per halo lane) instead of running the
                     // whole pipeline body on dummy loads -- idle helpers steal VALU issue slots
                     // from the compute waves sharing their SIMD.
                     if (__all(fA >= nsteps && hA >= P.A)) break;
-                    const int own_n = min(ST_G, min(nsteps - fA, prog + ST_RO - fA));
+                    const int own_n = min(ST_G, min(nsteps - fA, min(prog + ST_RO - fA, ST_CWA ? fCl - fA : ST_G)));
                     const int halo_n = hvalid ? min(ST_G, min(P.A - hA, prog + ST_RH - hoff - 2 - hA)) : 0;
-                    bool go = own_n > 0;
+                    bool go = own_n > 0 || (ST_CWA && fCl < min(nsteps, fA + ST_RC));
                     if (halo_n > 0)
                         go = go || hbound ||
                              st_granule_ready(__hip_atomic_load(hsrc + hA, __ATOMIC_RELAXED, GSCOPE), P.epoch);
@@ -1504,6 +1532,27 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 // pending (its per-use waits would otherwise serialise the gathers below).
                 asm volatile("s_waitcnt vmcnt(0)" : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(q0), "+v"(q1),
                              "+v"(q2), "+v"(q3)::"memory");
+#if ST_CWA
+                // the cell words that landed go to their slots; batch A = the next own steps with a word and a
+                // free own slot (a wave-uniform count), its words read back from LDS
+                if (0 < gCl) s_cw[(fCl & (ST_RC - 1)) * ST_NCOL + L] = c0;
+                if (1 < gCl) s_cw[((fCl + 1) & (ST_RC - 1)) * ST_NCOL + L] = c1;
+#if ST_G_DEF > 2
+                if (2 < gCl) s_cw[((fCl + 2) & (ST_RC - 1)) * ST_NCOL + L] = c2;
+                if (3 < gCl) s_cw[((fCl + 3) & (ST_RC - 1)) * ST_NCOL + L] = c3;
+#endif
+                fCl += gCl;
+                gA = max(0, min(ST_G, min(nsteps - fA, min(prog + ST_RO - fA, fCl - fA))));
+                const unsigned long long u0 = s_cw[(fA & (ST_RC - 1)) * ST_NCOL + L],
+                                         u1 = s_cw[((fA + 1) & (ST_RC - 1)) * ST_NCOL + L];
+#if ST_G_DEF > 2
+                const unsigned long long u2 = s_cw[((fA + 2) & (ST_RC - 1)) * ST_NCOL + L],
+                                         u3 = s_cw[((fA + 3) & (ST_RC - 1)) * ST_NCOL + L];
+#endif
+#define ST_OWNW(g) u##g
+#else
+#define ST_OWNW(g) c##g
+#endif
                 // ---- stage 2: vertices for batch A ----
                 int hp = 0;   // ready prefix of the halo batch (tag == epoch; boundary planes always)
                 const bool r0 = hbound || st_granule_ready(q0, P.epoch);
@@ -1514,21 +1563,8 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 #define ST_OWN_OK(g) ((g) < gA && col && fA + (g) - bl - cl >= 0 && fA + (g) - bl - cl < P.A)
 // (the role tests are conditional operators on ROLE, a constant with one helper wave: clang emits only the
 // live arm, so the one-helper code is the original's instruction for instruction)
-// ST_MASKED (A/B): the gathers and stage-1 loads only in the lanes that use them (exec-masked) instead of
-// every lane reading a dummy: a wave-wide load costs the texture addresser per lane
-#ifndef ST_MASKED
-#define ST_MASKED 0
-#endif
-#if ST_MASKED
-#define ST_GATHER(g, cg, qg)                                                                          \
-    const bool go##g = ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0, gh##g = (g) < hp && lbl_of((uint32_t)(qg)) >= 0; \
-    const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && go##g ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
-    const float4 oa##g = (ROLE != 2 && go##g) ? P.soup[so##g] : z4, ob##g = (ROLE != 2 && go##g) ? P.soup[so##g + 1] : z4, \
-                 oc##g = (ROLE != 2 && go##g) ? P.soup[so##g + 2] : z4;                                \
-    const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && gh##g ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
-    const float4 ha##g = (ROLE != 1 && gh##g) ? P.soup[sh##g] : z4, hb##g = (ROLE != 1 && gh##g) ? P.soup[sh##g + 1] : z4, \
-                 hc##g = (ROLE != 1 && gh##g) ? P.soup[sh##g + 2] : z4;
-#else
+// (exec-masking the gathers and stage-1 loads to the lanes that use them instead of a dummy read in every lane
+// measured slower: C3 first pass 10.5 -> 13.6 ms, C4 38.6 -> 42.0 ms)
 #define ST_GATHER(g, cg, qg)                                                                          \
     const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
     const float4 oa##g = ROLE != 2 ? P.soup[so##g] : z4, ob##g = ROLE != 2 ? P.soup[so##g + 1] : z4,    \
@@ -1536,17 +1572,20 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
     const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
     const float4 ha##g = ROLE != 1 ? P.soup[sh##g] : z4, hb##g = ROLE != 1 ? P.soup[sh##g + 1] : z4,    \
                  hc##g = ROLE != 1 ? P.soup[sh##g + 2] : z4;
-#endif
-                ST_GATHER(0, c0, q0)
-                ST_GATHER(1, c1, q1)
+                ST_GATHER(0, ST_OWNW(0), q0)
+                ST_GATHER(1, ST_OWNW(1), q1)
 #if ST_G_DEF > 2
-                ST_GATHER(2, c2, q2)
-                ST_GATHER(3, c3, q3)
+                ST_GATHER(2, ST_OWNW(2), q2)
+                ST_GATHER(3, ST_OWNW(3), q3)
 #endif
-                // ---- stage 1: issue batch B ----
+                // ---- stage 1: issue batch B (ST_CWA: the cell words of own steps [fI, fI + gI), up to ST_RC
+                //      steps past batch A) and the halo granules ----
                 const int fB = fA + gA;
-                int gB = min(ST_G, min(nsteps - fB, prog + ST_RO - fB));
-                if (gB < 0) gB = 0;
+#if ST_CWA
+                const int fI = fCl, gI = max(0, min(ST_G, min(nsteps - fI, fB + ST_RC - fI)));
+#else
+                const int fI = fB, gI = max(0, min(ST_G, min(nsteps - fB, prog + ST_RO - fB)));
+#endif
                 const int hB = hA + hp;
                 int hcB = 0;
                 if (hvalid) {
@@ -1555,14 +1594,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 }
 #define ST_ISSUE(g, cn, qn)                                                                            \
     {                                                                                                  \
-        const int a_ = fB + (g) - bl - cl;                                                             \
-        const bool ok_ = (g) < gB && col && a_ >= 0 && a_ < P.A;                                       \
+        const int a_ = fI + (g) - bl - cl;                                                             \
+        const bool ok_ = (g) < gI && col && a_ >= 0 && a_ < P.A;                                       \
         const size_t ix_ = (ok_ && ST_DIAG_SPLIT != 4) ? st_phys(P, a_, b, c) : dummy;                 \
-        cn = (ROLE != 2 && (!ST_MASKED || ok_)) ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;       \
+        cn = ROLE != 2 ? P.cell[SDF_CHK(6, ix_, P.clo, P.chi)] : ~0ull;                                \
         const unsigned long long *src_ =                                                               \
             (g) >= hcB ? P.cell + SDF_CHK(7, dummy, P.clo, P.chi)                                      \
                        : (hbound ? P.cell + SDF_CHK(10, st_phys(P, hB + (g), hbs, hcs), P.clo, P.chi) : hsrc + hB + (g)); \
-        qn = (ROLE != 1 && (!ST_MASKED || (g) < hcB)) ? __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE) : 0ull; \
+        qn = ROLE != 1 ? __hip_atomic_load(src_, __ATOMIC_RELAXED, GSCOPE) : 0ull;                     \
     }
                 // Always issued (a fixed count keeps the waits below precise); slots with nothing
                 // to fetch read a cached dummy, and idle helpers back off, so waiting tiles do
@@ -1583,30 +1622,32 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 // ---- land batch A in LDS, then publish readiness ----
 #define ST_LAND(g, cg, qg)                                                                             \
     if (ST_OWN_OK(g)) {                                                                                \
-        const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + L;                   \
+        const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + LR;                  \
         s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __uint_as_float((uint32_t)(cg)));      \
         s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
         s_ent[3 * e_ + 2] = oc##g;                                                                     \
     }                                                                                                  \
     if ((g) < hp) {                                                                                    \
-        const int e_ = ST_HALO0 + L * ST_RH + ((hA + (g)) & (ST_RH - 1));                              \
+        const int e_ = ST_HALO0 + LR * ST_RH + ((hA + (g)) & (ST_RH - 1));                             \
         s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __uint_as_float((uint32_t)(qg)));      \
         s_ent[3 * e_ + 1] = hb##g;                                                                     \
         s_ent[3 * e_ + 2] = hc##g;                                                                     \
     }
-                ST_LAND(0, c0, q0)
-                ST_LAND(1, c1, q1)
+                const int LR = ST_LANE_REMAT ? st_lane_remat() : L;   // (== L)
+                ST_LAND(0, ST_OWNW(0), q0)
+                ST_LAND(1, ST_OWNW(1), q1)
 #if ST_G_DEF > 2
-                ST_LAND(2, c2, q2)
-                ST_LAND(3, c3, q3)
+                ST_LAND(2, ST_OWNW(2), q2)
+                ST_LAND(3, ST_OWNW(3), q3)
 #endif
+#undef ST_OWNW
 #undef ST_OWN_OK
 #undef ST_GATHER
 #undef ST_ISSUE
 #undef ST_LAND
                 lds_drain();
                 if (L == 0 && gA) lds_st(&s_hdr[0], fB);
-                if (hvalid && hp) lds_st(&s_halo_ready[L], hB);
+                if (hvalid && hp) lds_st(&s_halo_ready[LR], hB);
                 if (TRACE && MULTI && P.trace) {   // [2] first halo entries landed, [4] first own entries landed
                     const bool h_now = __any(hvalid && hp > 0 && L < ST_T), o_now = gA > 0;   // b-edge streams (from J - 1)
                     if (h_now && !tr_halo && L == 0) P.trace[8 * task + 2] = wall_clock64();
@@ -1614,7 +1655,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     tr_halo |= h_now;
                     tr_own |= o_now;
                 }
-                const bool moved = gA > 0 || hp > 0 || gB > 0;   // a halo poll that lands nothing is idle
+                const bool moved = gA > 0 || hp > 0 || gI > 0;   // a halo poll that lands nothing is idle
 #ifdef ST_STEP_PROF
                 if (P.stats && __any(moved)) {
                     const unsigned long long t_ = clock64();
@@ -1627,10 +1668,11 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                     hp_t0 = t_;
                 }
 #endif
-                fA = fB; gA = gB; hA = hB; hcA = hcB;
+                fA = fB; hA = hB; hcA = hcB;
+                if (ST_CWA) gCl = gI; else gA = gI;
                 c0 = n0; c1 = n1; c2 = n2; c3 = n3;
                 q0 = m0; q1 = m1; q2 = m2; q3 = m3;
-                if (__all(fB >= nsteps && gB == 0 && hB >= P.A)) break;
+                if (__all(fB >= nsteps && (ST_CWA || gI == 0) && hB >= P.A)) break;
                 if (__any(moved)) {
                     idle = 0;
                 } else {
