@@ -73,6 +73,9 @@ namespace sdfhip {
 #ifndef ST_RC_DEF
 #define ST_RC_DEF 8    // ST_CWA: own cell-word slots (power of two)
 #endif
+#ifndef ST_COMPUTE_WAIT0
+#define ST_COMPUTE_WAIT0 1
+#endif
 #ifndef ST_WORK_PRIO
 #define ST_WORK_PRIO 2   // compute waves' issue priority while stepping (0 while they wait)
 #endif
@@ -582,6 +585,12 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         if (TRACE && P.trace && tid == 0) P.trace[8 * task] = wall_clock64();
         if (wave < ST_NCW) {
             // ======================= compute waves =======================
+            // Nothing of this wave is in flight here (the task's set-up loads were consumed above).  Said with the
+            // builtin, not an asm, so the compiler's wait-count pass knows it: its scoreboard is per function, and
+            // without this it carried the helper branch's pending load registers (a role the same wave never takes)
+            // into the step loop, where the 1-wave tiles then waited for their own previous step's granule and
+            // cell stores (vmcnt(0) in every evaluation pass) (ST_COMPUTE_WAIT0)
+            if (ST_COMPUTE_WAIT0) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0), expcnt / lgkmcnt unchanged (gfx9 encoding)
             // Wave w owns the ST_CLW c-columns from ST_CLW * w on: lanes 0..31 are its 32 cells.
             // Wave w steps h only after wave w-1 finished step h-1 (its column cl-1 results) and
             // at most RR-4 steps ahead of wave w+1 (ring slots).  TWIN: lane L + 32 is the twin
