@@ -73,6 +73,9 @@ namespace sdfhip {
 #ifndef ST_RC_DEF
 #define ST_RC_DEF 8    // ST_CWA: own cell-word slots (power of two)
 #endif
+#ifndef ST_HALO_FIRST
+#define ST_HALO_FIRST 1   // helper: the halo batch's gathers issued, landed and published before the own batch's
+#endif
 #ifndef ST_COMPUTE_WAIT0
 #define ST_COMPUTE_WAIT0 1
 #endif
@@ -1574,18 +1577,39 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
 // live arm, so the one-helper code is the original's instruction for instruction)
 // (exec-masking the gathers and stage-1 loads to the lanes that use them instead of a dummy read in every lane
 // measured slower: C3 first pass 10.5 -> 13.6 ms, C4 38.6 -> 42.0 ms)
-#define ST_GATHER(g, cg, qg)                                                                          \
+#define ST_GATHER_O(g, cg)                                                                             \
     const size_t so##g = 3 * SDF_CHK(11, (ST_DIAG_SPLIT != 2 && ST_OWN_OK(g) && lbl_of((uint32_t)(cg)) >= 0 ? lbl_of((uint32_t)(cg)) : gdum), 0, P.ntri); \
     const float4 oa##g = ROLE != 2 ? P.soup[so##g] : z4, ob##g = ROLE != 2 ? P.soup[so##g + 1] : z4,    \
-                 oc##g = ROLE != 2 ? P.soup[so##g + 2] : z4;                                           \
+                 oc##g = ROLE != 2 ? P.soup[so##g + 2] : z4;
+#define ST_GATHER_H(g, qg)                                                                             \
     const size_t sh##g = 3 * SDF_CHK(12, (ST_DIAG_SPLIT != 3 && (g) < hp && lbl_of((uint32_t)(qg)) >= 0 ? lbl_of((uint32_t)(qg)) : gdum), 0, P.ntri); \
     const float4 ha##g = ROLE != 1 ? P.soup[sh##g] : z4, hb##g = ROLE != 1 ? P.soup[sh##g + 1] : z4,    \
                  hc##g = ROLE != 1 ? P.soup[sh##g + 2] : z4;
-                ST_GATHER(0, ST_OWNW(0), q0)
-                ST_GATHER(1, ST_OWNW(1), q1)
+#if ST_HALO_FIRST
+                // the halo batch's gathers first: its landing then waits for them alone (loads return in order)
+                ST_GATHER_H(0, q0)
+                ST_GATHER_H(1, q1)
 #if ST_G_DEF > 2
-                ST_GATHER(2, ST_OWNW(2), q2)
-                ST_GATHER(3, ST_OWNW(3), q3)
+                ST_GATHER_H(2, q2)
+                ST_GATHER_H(3, q3)
+#endif
+                ST_GATHER_O(0, ST_OWNW(0))
+                ST_GATHER_O(1, ST_OWNW(1))
+#if ST_G_DEF > 2
+                ST_GATHER_O(2, ST_OWNW(2))
+                ST_GATHER_O(3, ST_OWNW(3))
+#endif
+#else
+                ST_GATHER_O(0, ST_OWNW(0))
+                ST_GATHER_H(0, q0)
+                ST_GATHER_O(1, ST_OWNW(1))
+                ST_GATHER_H(1, q1)
+#if ST_G_DEF > 2
+                ST_GATHER_O(2, ST_OWNW(2))
+                ST_GATHER_H(2, q2)
+                ST_GATHER_O(3, ST_OWNW(3))
+                ST_GATHER_H(3, q3)
+#endif
 #endif
                 // ---- stage 1: issue batch B (ST_CWA: the cell words of own steps [fI, fI + gI), up to ST_RC
                 //      steps past batch A) and the halo granules ----
@@ -1629,13 +1653,14 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
                 if (__any(hp > 0)) __builtin_amdgcn_s_sleep(ST_HALO_DELAY);
 #endif
                 // ---- land batch A in LDS, then publish readiness ----
-#define ST_LAND(g, cg, qg)                                                                             \
+#define ST_LAND_O(g, cg)                                                                               \
     if (ST_OWN_OK(g)) {                                                                                \
         const int e_ = ST_OWN0 + ((fA + (g) - bl - cl) & (ST_RO - 1)) * ST_NCOL + LR;                  \
         s_ent[3 * e_] = make_float4(oa##g.x, oa##g.y, oa##g.z, __uint_as_float((uint32_t)(cg)));      \
         s_ent[3 * e_ + 1] = make_float4(ob##g.x, ob##g.y, ob##g.z, __uint_as_float((uint32_t)((cg) >> 32))); \
         s_ent[3 * e_ + 2] = oc##g;                                                                     \
-    }                                                                                                  \
+    }
+#define ST_LAND_H(g, qg)                                                                               \
     if ((g) < hp) {                                                                                    \
         const int e_ = ST_HALO0 + LR * ST_RH + ((hA + (g)) & (ST_RH - 1));                             \
         s_ent[3 * e_] = make_float4(ha##g.x, ha##g.y, ha##g.z, __uint_as_float((uint32_t)(qg)));      \
@@ -1643,20 +1668,47 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
         s_ent[3 * e_ + 2] = hc##g;                                                                     \
     }
                 const int LR = ST_LANE_REMAT ? st_lane_remat() : L;   // (== L)
-                ST_LAND(0, ST_OWNW(0), q0)
-                ST_LAND(1, ST_OWNW(1), q1)
+#if ST_HALO_FIRST
+                // the halo entries land and are published as soon as their gathers are back (the tile hop is
+                // on the critical path: DESIGN.md §6), then the own entries
+                ST_LAND_H(0, q0)
+                ST_LAND_H(1, q1)
 #if ST_G_DEF > 2
-                ST_LAND(2, ST_OWNW(2), q2)
-                ST_LAND(3, ST_OWNW(3), q3)
+                ST_LAND_H(2, q2)
+                ST_LAND_H(3, q3)
 #endif
-#undef ST_OWNW
-#undef ST_OWN_OK
-#undef ST_GATHER
-#undef ST_ISSUE
-#undef ST_LAND
+                lds_drain();
+                if (hvalid && hp) lds_st(&s_halo_ready[LR], hB);
+                ST_LAND_O(0, ST_OWNW(0))
+                ST_LAND_O(1, ST_OWNW(1))
+#if ST_G_DEF > 2
+                ST_LAND_O(2, ST_OWNW(2))
+                ST_LAND_O(3, ST_OWNW(3))
+#endif
+                lds_drain();
+                if (L == 0 && gA) lds_st(&s_hdr[0], fB);
+#else
+                ST_LAND_O(0, ST_OWNW(0))
+                ST_LAND_H(0, q0)
+                ST_LAND_O(1, ST_OWNW(1))
+                ST_LAND_H(1, q1)
+#if ST_G_DEF > 2
+                ST_LAND_O(2, ST_OWNW(2))
+                ST_LAND_H(2, q2)
+                ST_LAND_O(3, ST_OWNW(3))
+                ST_LAND_H(3, q3)
+#endif
                 lds_drain();
                 if (L == 0 && gA) lds_st(&s_hdr[0], fB);
                 if (hvalid && hp) lds_st(&s_halo_ready[LR], hB);
+#endif
+#undef ST_OWNW
+#undef ST_OWN_OK
+#undef ST_GATHER_O
+#undef ST_GATHER_H
+#undef ST_ISSUE
+#undef ST_LAND_O
+#undef ST_LAND_H
                 if (TRACE && MULTI && P.trace) {   // [2] first halo entries landed, [4] first own entries landed
                     const bool h_now = __any(hvalid && hp > 0 && L < ST_T), o_now = gA > 0;   // b-edge streams (from J - 1)
                     if (h_now && !tr_halo && L == 0) P.trace[8 * task + 2] = wall_clock64();
