@@ -76,6 +76,9 @@ namespace sdfhip {
 #ifndef ST_HALO_FIRST
 #define ST_HALO_FIRST 1   // helper: the halo batch's gathers issued, landed and published before the own batch's
 #endif
+#ifndef ST_HELPER_PRIO
+#define ST_HELPER_PRIO 0   // the helper wave's issue priority (the compute waves step at ST_WORK_PRIO)
+#endif
 #ifndef ST_COMPUTE_WAIT0
 #define ST_COMPUTE_WAIT0 1
 #endif
@@ -1446,6 +1449,7 @@ __global__ void __launch_bounds__(Cfg::THREADS, Cfg::WPE) k_sweep_tile(StParams 
             // tests fold away and the code is the one-helper loop instruction for instruction -- a lambda per role
             // cost the default build 2 % in register allocation, round 5.)
             const int ROLE = Cfg::NH == 1 ? 0 : (wave == ST_NCW ? 1 : 2);
+            if (ST_HELPER_PRIO) __builtin_amdgcn_s_setprio(ST_HELPER_PRIO);
             const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
             const int bl = L & (ST_T - 1), cl = L >> 3;   // helper lane L prefetches column (bl, cl)
             const int b = b0 + bl, c = c0 + cl;
