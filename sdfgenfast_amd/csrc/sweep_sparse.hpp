@@ -152,6 +152,10 @@ static_assert(!SP_BUSY_NO_TAIL || SP_DIRECT_POLL, "skipping the tail read needs 
                           // (profiles/r06g_ab_jscan_c{3,4}.log): C4 11.05 (0) / 10.44 (1) / 10.43-10.46 ms (2),
                           // C3 2.60 / 2.66 / 2.57-2.60 ms; scan launch C4 630 -> 518 us (2)
 #endif
+#ifndef SP_JSCAN_K
+#define SP_JSCAN_K 1   // the pair scan streaming along k (k_sp_jscan3): two pair loads per plane instead of four;
+                       // SDFGEN_JSCAN_K=0 (diagnostics) runs k_sp_jscan2
+#endif
 #ifndef SP_JACOBI_CHUNK
 #define SP_JACOBI_CHUNK 1   // k_sp_jacobi: a contiguous chunk per block (L2 reuse of the upwind plane)
 #endif
@@ -1002,6 +1006,160 @@ __global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan2(SpParams P)
         const int cj = j >= P.nj;
         j -= cj ? P.nj : 0;
         k += sk + cj;
+    }
+    if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
+}
+
+// The pair scan streaming along k (SP_JSCAN_K).  k_sp_jscan2 loads four pair streams per lane: its own, the
+// j-upwind row's, the k-upwind plane's and the jk diagonal's; the last two are the first two of the plane
+// before.  Here a wave owns one row segment of 64 x 2 NP cells (i) and walks a chunk of KC planes in the
+// sweep's k order, upwind first, so the plane it needs as k-upwind is the one it held in the previous
+// iteration: its k and jk pairs are the previous O and Jp (registers), and a plane costs two pair loads per
+// lane instead of four (the chunk's first plane: four).  The j-upwind row is the block's next wave's own row
+// (a workgroup is 4 consecutive rows), loaded again from L1 / L2.  Blocks: XCD x = blockIdx % 8 takes the
+// x-th eighth of the (k-chunk, row group, segment) items, so a block's neighbours are on its XCD.  Same
+// decision (sp_any_scan) for the same cells, so the same list SET as k_sp_jacobi's; its order is per row
+// segment and plane (k_sp_jlist evaluates each listed cell independently, and the repair's result does not
+// depend on the order of its requests: the header's uniqueness argument).
+struct SpKGeom {
+    unsigned nseg, nrg, kc, items, per_xcd;   // row segments per row, row groups (4 rows), planes per chunk, items
+};
+inline SpKGeom sp_kgeom(int ni, int nj, int nk, int np)
+{
+    SpKGeom G;
+    const unsigned rw = 128u * (unsigned)np;
+    G.nseg = ((unsigned)ni + rw - 1) / rw;
+    G.nrg = ((unsigned)nj + 3) / 4;
+    // about 16,384 items, 4..64 planes each: at C4 8 planes per chunk (scan + list pass per sweep, rocprof:
+    // 4 planes 453 + 336, 8 planes 435 + 338, 32 planes 444 + 340, 128 planes 557 + 393 us; k_sp_jscan2 521 + 309,
+    // profiles/r06o_kc_c4.txt); C3 takes the minimum, 4
+    const unsigned long long cols = (unsigned long long)G.nseg * G.nrg;
+    G.kc = (unsigned)std::max<unsigned long long>(4, std::min<unsigned long long>(64, cols * (unsigned long long)nk / 16384));
+    if (const char *e = getenv("SDFGEN_JSCAN_KC")) G.kc = (unsigned)std::max(1, std::min(nk, atoi(e)));   // (diagnostics)
+    G.items = (unsigned)(((unsigned long long)nk + G.kc - 1) / G.kc * cols);
+    G.per_xcd = (G.items + 7) / 8;
+    return G;
+}
+inline unsigned long long sp_kgeom_cells_per_block(const SpKGeom &G, int np) { return (unsigned long long)G.kc * 4 * 128 * np; }
+
+template <int NP>
+__global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan3(SpParams P, SpKGeom G)
+{
+    __shared__ unsigned s_list[4][SP_JWAVE];
+    const unsigned lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const unsigned part = blockIdx.x % SP_JPARTS;   // part % 8 = this block's XCD (k_sp_jlist's blocks of the part run there)
+    unsigned *buf = s_list[wv];
+    unsigned cnt = 0;   // wave-uniform
+    constexpr unsigned CL = 2 * NP, RW = 64 * CL;
+    const unsigned item = (blockIdx.x % 8) * G.per_xcd + blockIdx.x / 8;
+    const int j = (int)((item / G.nseg) % G.nrg) * 4 + (int)wv;   // this wave's row
+    if (item >= G.items || j >= P.nj) return;   // (no workgroup barrier below: a wave may leave)
+    const unsigned seg = item % G.nseg, kch = item / (G.nseg * G.nrg);
+    const int i0 = (int)(seg * RW + CL * lane);   // the lane's first cell in the row
+    const bool lane_in = i0 < P.ni;                // lanes past the row end load the wave's first pair (never used)
+    const long long dJ = -(long long)P.dj * P.ni, dK = -(long long)P.dk * P.ni * P.nj;   // pair offsets (cells)
+    const bool hasJ = (unsigned)(j - P.dj) < (unsigned)P.nj;   // the j-upwind row exists (else no cell of it is in range)
+    const char *bS = (const char *)P.S, *bJ = (const char *)(P.S + dJ), *bK = (const char *)(P.S + dK),
+               *bJK = (const char *)(P.S + dJ + dK);   // (scalar bases; a base may lie outside the buffer)
+    const bool pos = P.di > 0;
+    const long long dI = pos ? -1ll : (long long)CL;   // the edge lane's own fetch: cell c + dI
+    const unsigned ip = (unsigned)(pos ? i0 : i0 + CL - 1);   // (unused: keeps the edge cell's row test cheap)
+    (void)ip;
+    sp_u32x4 O[NP], Jp[NP], Kp[NP], JK[NP];
+    uint32_t e0 = 0u, e1 = 0u, e2 = 0u, e3 = 0u;   // the edge lane's i-upwind words (O, J, K, JK)
+    const int kk0 = (int)(kch * G.kc), kk1 = min(P.nk, kk0 + (int)G.kc);
+    for (int kk = kk0; kk < kk1; ++kk) {   // wave-uniform
+        const int k = P.dk > 0 ? kk : P.nk - 1 - kk;   // planes in the sweep's order: upwind first
+        const long long crow = (long long)P.ni * (j + (long long)P.nj * k);   // the row's first cell
+        const unsigned long long c = (unsigned long long)(crow + (lane_in ? i0 : (int)(seg * RW)));
+        const uint32_t boff = (uint32_t)c << 3;   // c < 2^29
+        (void)SDF_CHK(20, c, 0, P.n + SP_PAD);
+        const bool first = kk == kk0;
+        const bool hasK = (unsigned)(k - P.dk) < (unsigned)P.nk;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            if (!first) { Kp[p] = O[p]; JK[p] = Jp[p]; }
+            O[p] = *(const sp_u32x4 *)(bS + boff + 16 * p);
+            Jp[p] = hasJ ? *(const sp_u32x4 *)(bJ + boff + 16 * p) : sp_u32x4{0u, 0u, 0u, 0u};
+            if (first) {
+                Kp[p] = hasK ? *(const sp_u32x4 *)(bK + boff + 16 * p) : sp_u32x4{0u, 0u, 0u, 0u};
+                JK[p] = (hasK && hasJ) ? *(const sp_u32x4 *)(bJK + boff + 16 * p) : sp_u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+        if (lane == (pos ? 0u : 63u)) {
+            const long long x = (long long)c + dI;
+            auto ld1 = [&](long long y) -> uint32_t {
+                return (y >= 0 && y < (long long)P.n) ? (uint32_t)P.S[SDF_CHK(22, y, 0, P.n)] : 0u;
+            };
+            if (!first) { e2 = e0; e3 = e1; }
+            e0 = ld1(x);
+            e1 = hasJ ? ld1(x + dJ) : 0u;
+            if (first) {
+                e2 = hasK ? ld1(x + dK) : 0u;
+                e3 = (hasK && hasJ) ? ld1(x + dJ + dK) : 0u;
+            }
+        }
+        uint32_t t0, t1, t2, t3;
+        if (pos) {   // wave_shr:1 -- lane L takes lane L - 1's last cell; lane 0 keeps its own fetch
+            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O[NP - 1].z, 0x138, 0xf, 0xf, false);
+            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp[NP - 1].z, 0x138, 0xf, 0xf, false);
+            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp[NP - 1].z, 0x138, 0xf, 0xf, false);
+            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK[NP - 1].z, 0x138, 0xf, 0xf, false);
+        } else {     // wave_shl:1 -- lane L takes lane L + 1's first cell; lane 63 keeps its own fetch
+            t0 = (uint32_t)__builtin_amdgcn_update_dpp((int)e0, (int)O[0].x, 0x130, 0xf, 0xf, false);
+            t1 = (uint32_t)__builtin_amdgcn_update_dpp((int)e1, (int)Jp[0].x, 0x130, 0xf, 0xf, false);
+            t2 = (uint32_t)__builtin_amdgcn_update_dpp((int)e2, (int)Kp[0].x, 0x130, 0xf, 0xf, false);
+            t3 = (uint32_t)__builtin_amdgcn_update_dpp((int)e3, (int)JK[0].x, 0x130, 0xf, 0xf, false);
+        }
+        unsigned f[CL];
+        const bool jk_in = (P.dj > 0 ? j >= 1 : j <= P.nj - 2) && (P.dk > 0 ? k >= 1 : k <= P.nk - 2);
+        const bool jk_interior = j >= 1 && j <= P.nj - 2 && k >= 1 && k <= P.nk - 2;
+#pragma unroll
+        for (int m = 0; m < CL; ++m) {
+            const int p = m >> 1;
+            const bool hi = m & 1;
+            const int ic = i0 + m;
+            const uint32_t wo = hi ? O[p].z : O[p].x, wj = hi ? Jp[p].z : Jp[p].x, wk = hi ? Kp[p].z : Kp[p].x,
+                           wjk = hi ? JK[p].z : JK[p].x;
+            uint32_t ui, uj, uk, ujk;   // the i-upwind cell's words
+            if (pos) {
+                if (m == 0) { ui = t0; uj = t1; uk = t2; ujk = t3; }
+                else if (hi) { ui = O[p].x; uj = Jp[p].x; uk = Kp[p].x; ujk = JK[p].x; }
+                else { ui = O[p - 1].z; uj = Jp[p - 1].z; uk = Kp[p - 1].z; ujk = JK[p - 1].z; }
+            } else {
+                if (m == CL - 1) { ui = t0; uj = t1; uk = t2; ujk = t3; }
+                else if (!hi) { ui = O[p].z; uj = Jp[p].z; uk = Kp[p].z; ujk = JK[p].z; }
+                else { ui = O[p + 1].x; uj = Jp[p + 1].x; uk = Kp[p + 1].x; ujk = JK[p + 1].x; }
+            }
+            const bool v = lane_in && ic < P.ni;
+            f[m] = 0u;
+            if (v && jk_in && (pos ? ic >= 1 : ic <= P.ni - 2)) {
+                const uint32_t w[7] = {ui, wj, uj, wk, uk, wjk, ujk};
+                const bool interior = jk_interior && ic >= 1 && ic <= P.ni - 2;
+                f[m] = sp_any_scan(P, wo, w, interior) ? 1u : 0u;
+            }
+            if (!P.sv && v && !f[m])   // two buffers: cells that keep their value are copied (in place they hold it)
+                P.X[c + m] = ((unsigned long long)(hi ? O[p].w : O[p].y) << 32) | wo;
+        }
+        // the list: lane L's cells after those of lanes < L (the row segment in address order)
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        unsigned at = cnt, tot = 0;
+#pragma unroll
+        for (int m = 0; m < CL; ++m) {
+            const unsigned long long bm = __ballot(f[m] != 0u);
+            at += (unsigned)__builtin_popcountll(bm & lt);
+            tot += (unsigned)__builtin_popcountll(bm);
+        }
+#pragma unroll
+        for (int m = 0; m < CL; ++m) {
+            if (f[m]) buf[at] = (unsigned)(c + m);
+            at += f[m];
+        }
+        cnt += tot;
+        if (cnt > SP_JWAVE - 64 * CL) {
+            sp_jlist_flush(P, part, buf, cnt, lane);
+            cnt = 0;
+        }
     }
     if (cnt) sp_jlist_flush(P, part, buf, cnt, lane);
 }
@@ -1886,7 +2044,13 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     // it for the ~10 % that are listed would need an in-place fallback whose registers
     // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
-    const unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
+    unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
+    if (c_lo == 0 && n == (unsigned long long)ni * nj * nk && n <= (1ull << 29)) {   // the k-streaming scan's blocks too
+        for (int np = 1; np <= 2; ++np) {
+            const SpKGeom G = sp_kgeom(ni, nj, nk, np);
+            jcap = std::max(jcap, (8ull * G.per_xcd + SP_JPARTS - 1) / SP_JPARTS * sp_kgeom_cells_per_block(G, np));
+        }
+    }
     if (int rc_ = sp_grow(&W.jlist, &W.cap_jlist, SP_JPARTS * jcap, false, st)) return rc_;
     memset(&P, 0, sizeof(P));
     P.soup = soup;
@@ -1933,7 +2097,13 @@ inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const Sp
     if (SP_JSCAN_FAST && P.c_lo == 0 && P.n == (unsigned long long)P.ni * P.nj * P.nk && P.k_lo == 0 && P.k_hi == P.nk &&
         P.n <= (1ull << 29) && blocks % 8 == 0) {
         static const int np = getenv("SDFGEN_JSCAN_NP") ? atoi(getenv("SDFGEN_JSCAN_NP")) : SP_JSCAN_PAIR;
-        if (np == 2) hipLaunchKernelGGL(k_sp_jscan2<2>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+        static const bool ks = getenv("SDFGEN_JSCAN_K") ? atoi(getenv("SDFGEN_JSCAN_K")) != 0 : SP_JSCAN_K != 0;
+        if (ks && (np == 1 || np == 2)) {
+            const SpKGeom G = sp_kgeom(P.ni, P.nj, P.nk, np);
+            if (np == 2) hipLaunchKernelGGL(k_sp_jscan3<2>, dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
+            else hipLaunchKernelGGL(k_sp_jscan3<1>, dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
+        }
+        else if (np == 2) hipLaunchKernelGGL(k_sp_jscan2<2>, dim3((unsigned)blocks), dim3(256), 0, st, P);
         else if (np == 1) hipLaunchKernelGGL(k_sp_jscan2<1>, dim3((unsigned)blocks), dim3(256), 0, st, P);
         else
             hipLaunchKernelGGL((k_sp_jacobi<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
