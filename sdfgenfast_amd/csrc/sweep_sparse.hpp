@@ -1041,8 +1041,13 @@ inline SpKGeom sp_kgeom(int ni, int nj, int nk, int np)
     return G;
 }
 inline unsigned long long sp_kgeom_cells_per_block(const SpKGeom &G, int np) { return (unsigned long long)G.kc * 4 * 128 * np; }
+// the k-streaming scan runs on a whole grid on one device whose cell indices fit the list's 32 bits
+inline bool sp_kscan_ok(unsigned long long c_lo, unsigned long long n, int ni, int nj, int nk)
+{
+    return SP_JSCAN_FAST && c_lo == 0 && n == (unsigned long long)ni * nj * nk && n + SP_PAD < (1ull << 32);
+}
 
-template <int NP>
+template <int NP, bool WIDE>   // WIDE: 64-bit byte offsets (grids above 2^29 cells: C5)
 __global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan3(SpParams P, SpKGeom G)
 {
     __shared__ unsigned s_list[4][SP_JWAVE];
@@ -1072,7 +1077,8 @@ __global__ void __launch_bounds__(256, NP == 1 ? 1 : 6) k_sp_jscan3(SpParams P, 
         const int k = P.dk > 0 ? kk : P.nk - 1 - kk;   // planes in the sweep's order: upwind first
         const long long crow = (long long)P.ni * (j + (long long)P.nj * k);   // the row's first cell
         const unsigned long long c = (unsigned long long)(crow + (lane_in ? i0 : (int)(seg * RW)));
-        const uint32_t boff = (uint32_t)c << 3;   // c < 2^29
+        const uint32_t boff32 = (uint32_t)c << 3;   // (c < 2^29 unless WIDE)
+        const unsigned long long boff = WIDE ? c << 3 : (unsigned long long)boff32;
         (void)SDF_CHK(20, c, 0, P.n + SP_PAD);
         const bool first = kk == kk0;
         const bool hasK = (unsigned)(k - P.dk) < (unsigned)P.nk;
@@ -2045,7 +2051,7 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     // (ptd) halve the scan's occupancy: 150 -> 108 us per sweep at 256^3 without it
     const unsigned long long per_block = ((n + 7) / 8 + blocks / 8 * 256 - 1) / (blocks / 8 * 256) * 256;
     unsigned long long jcap = (blocks + SP_JPARTS - 1) / SP_JPARTS * per_block;
-    if (c_lo == 0 && n == (unsigned long long)ni * nj * nk && n <= (1ull << 29)) {   // the k-streaming scan's blocks too
+    if (sp_kscan_ok(c_lo, n, ni, nj, nk)) {   // the k-streaming scan's blocks too
         for (int np = 1; np <= 2; ++np) {
             const SpKGeom G = sp_kgeom(ni, nj, nk, np);
             jcap = std::max(jcap, (8ull * G.per_xcd + SP_JPARTS - 1) / SP_JPARTS * sp_kgeom_cells_per_block(G, np));
@@ -2091,19 +2097,25 @@ inline int sp_setup(SparseSweepWorkspace &W, hipStream_t st, const float4 *soup,
     return 0;
 }
 
-// the one-device scan, in its fast form where the byte offsets fit 32 bits
+// the one-device scan: the k-streaming pair scan on a whole grid (64-bit offsets above 2^29 cells), the
+// other fast forms where the byte offsets fit 32 bits
 inline void sp_launch_jacobi(unsigned long long blocks, hipStream_t st, const SpParams &P)
 {
-    if (SP_JSCAN_FAST && P.c_lo == 0 && P.n == (unsigned long long)P.ni * P.nj * P.nk && P.k_lo == 0 && P.k_hi == P.nk &&
-        P.n <= (1ull << 29) && blocks % 8 == 0) {
-        static const int np = getenv("SDFGEN_JSCAN_NP") ? atoi(getenv("SDFGEN_JSCAN_NP")) : SP_JSCAN_PAIR;
-        static const bool ks = getenv("SDFGEN_JSCAN_K") ? atoi(getenv("SDFGEN_JSCAN_K")) != 0 : SP_JSCAN_K != 0;
-        if (ks && (np == 1 || np == 2)) {
-            const SpKGeom G = sp_kgeom(P.ni, P.nj, P.nk, np);
-            if (np == 2) hipLaunchKernelGGL(k_sp_jscan3<2>, dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
-            else hipLaunchKernelGGL(k_sp_jscan3<1>, dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
+    static const int np = getenv("SDFGEN_JSCAN_NP") ? atoi(getenv("SDFGEN_JSCAN_NP")) : SP_JSCAN_PAIR;
+    static const bool ks = getenv("SDFGEN_JSCAN_K") ? atoi(getenv("SDFGEN_JSCAN_K")) != 0 : SP_JSCAN_K != 0;
+    if (ks && (np == 1 || np == 2) && sp_kscan_ok(P.c_lo, P.n, P.ni, P.nj, P.nk) && P.k_lo == 0 && P.k_hi == P.nk) {
+        const SpKGeom G = sp_kgeom(P.ni, P.nj, P.nk, np);
+        const bool wide = P.n > (1ull << 29);
+        if (np == 2) {
+            if (wide) hipLaunchKernelGGL((k_sp_jscan3<2, true>), dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
+            else hipLaunchKernelGGL((k_sp_jscan3<2, false>), dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
+        } else {
+            if (wide) hipLaunchKernelGGL((k_sp_jscan3<1, true>), dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
+            else hipLaunchKernelGGL((k_sp_jscan3<1, false>), dim3(8 * G.per_xcd), dim3(256), 0, st, P, G);
         }
-        else if (np == 2) hipLaunchKernelGGL(k_sp_jscan2<2>, dim3((unsigned)blocks), dim3(256), 0, st, P);
+    } else if (SP_JSCAN_FAST && P.c_lo == 0 && P.n == (unsigned long long)P.ni * P.nj * P.nk && P.k_lo == 0 && P.k_hi == P.nk &&
+        P.n <= (1ull << 29) && blocks % 8 == 0) {
+        if (np == 2) hipLaunchKernelGGL(k_sp_jscan2<2>, dim3((unsigned)blocks), dim3(256), 0, st, P);
         else if (np == 1) hipLaunchKernelGGL(k_sp_jscan2<1>, dim3((unsigned)blocks), dim3(256), 0, st, P);
         else
             hipLaunchKernelGGL((k_sp_jacobi<false, true>), dim3((unsigned)blocks), dim3(256), 0, st, P);
