@@ -24,18 +24,19 @@ uncached system-scope round trip is 0.82 us, tools/uc_lat).
 """
 import json
 
-# ---- measured inputs (one MI355X, round 5) ----
+# ---- measured inputs (one MI355X, round 6 final build 6c8f290b) ----
 INPUTS = {
-    "c3_sphere1m_256": {   # bench r05y (build 9e941c33): 13.71 ms in phases; tile launch 10.23 ms; 8 sparse sweeps 2.72 ms
-        "dims": (256, 256, 256), "t_local": 0.7504, "t_first": 10.2276, "t_second": 2.7227,
-        "t_repair_per_sweep": 0.2116,  # k_sp_recheck per sweep at C3 (profiles/r05y_c3_kernel_stats.csv, 8 x 6 calls)
+    "c3_sphere1m_256": {   # bench r06z: 13.45 ms in phases; tile launch 10.25 ms (rocprof avg); 8 sparse sweeps 2.53 ms
+        "dims": (256, 256, 256), "t_local": 0.7238, "t_first": 10.2500, "t_second": 2.5334,
+        "t_repair_per_sweep": 0.2113,  # k_sp_recheck per sweep at C3 (profiles/r06z_c3_kernel_stats.csv, 8 x 6 calls)
         "t_first_work": 5.0,           # tile work at full throughput: C4's first pass x 1/8 of the cells
         "longest_chain": 86,           # longest relabel chain of a second-pass sweep (oracle)
     },
-    "c4_sphere1m_512": {   # round 5 A/B (profiles/r05w_ab_vmask_c4.log): 53.7 ms; tile 40.15 ms; sparse 11.40 ms
-        "dims": (512, 512, 512), "t_local": 2.15, "t_first": 40.15, "t_second": 11.40,
+    "c4_sphere1m_512": {   # round 6 (bench r06z zslab_c4: 51.56 ms in phases; tile 38.44 ms rocprof avg,
+        # profiles/r06z_c4_kernel_stats.csv; sparse 10.30 ms)
+        "dims": (512, 512, 512), "t_local": 1.883, "t_first": 38.44, "t_second": 10.297,
         "t_repair_per_sweep": 0.62,    # repair_ms per sweep, 2-slab rehearsal (r03c_n2 zslab_c4), median
-        "t_first_work": 40.15,         # throughput-bound at one GPU: the launch itself
+        "t_first_work": 38.44,         # throughput-bound at one GPU: the launch itself
         "longest_chain": 172,          # not measured at C4: 2 x C3's (chains scale with the grid edge)
         # round 5, one MI355X (profiles/r05d_sparse_from_c4.log, SDFGEN_SPARSE_FROM=k, per-sweep events): the
         # first pass's last sweeps as Jacobi + repair instead of inside the tile launch -- the tile launch of the
@@ -45,7 +46,7 @@ INPUTS = {
                         6: {"tile": 32.296, "sparse_first": [30.297, 37.807]}},
     },
 }
-S_ISO_US = 1.088     # isolated tile step, quad-lane tiles (round 5 latency probe, 1024x9x9 grid: profiles/r05z_steplat_qvm.log)
+S_ISO_US = 1.056     # isolated tile step, quad-lane tiles (round 6 bench latency probe, 1024x9x9 grid: profiles/r06z_c3_bench.json.log)
 H_X_US = 2.0         # cross-GPU granule hand-off over xGMI (assumed; on-chip uncached round trip 0.82 us)
 H_FLAG_US = 2.0      # one DONE / READY flag hand-off between neighbour GPUs (assumed, as h_x)
 LINK_IDLE_US = 1.25  # one repair chain link on an idle chip: ~4 returning atomics + 2 dependent loads, ~3,000 cycles
@@ -137,7 +138,7 @@ def gs_levels(ni, nj, nk, nsw=8):
     return int(L.max())
 
 
-def ceiling(name, inp, steps_us=(1.088, 0.75, 0.49, 0.38), n=8):
+def ceiling(name, inp, steps_us=(1.056, 0.75, 0.49, 0.38), n=8):
     """the N-GPU efficiency this design could reach with a shorter isolated step.  First
     pass = max(levels x s, work / N) (crowding as in predict); second pass with the measured repair (does
     not shrink with N) and with every repair link at its idle-chip latency (the best case)."""
