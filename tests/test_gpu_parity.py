@@ -232,6 +232,26 @@ def test_gpu_sweep_impls_small_and_ragged_grids(sweep_impl, dims):
     assert bits_equal(got, want), diff_report(got, want, dx)
 
 
+# The second pass's k-streaming pair scan (sweep_sparse.hpp k_sp_jscan3) cuts each row into segments of
+# 64 x 2 NP cells, groups 4 rows per workgroup and walks chunks of planes: rows of several segments with a
+# partial last one (the lanes past the row end, the DPP hand-off across a segment edge in both i
+# directions), row groups and plane chunks that do not divide the grid.
+@pytest.mark.parametrize("dims", [(300, 9, 11), (513, 5, 7), (257, 6, 13)])
+@pytest.mark.parametrize("mode", ["hybrid", "sparse"])
+def test_gpu_second_pass_scan_row_segments(mode, dims, monkeypatch):
+    for k in ("SDFGEN_SWEEP", "SDFGEN_SPARSE_FROM", "SDFGEN_SPARSE_BRICK", "SDFGEN_SPARSE_INPLACE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, val in SWEEP_MODES[mode][0].items():
+        monkeypatch.setenv(k, val)
+    v, t = meshgen.bumpy_sphere(60, 23)
+    o, dx = meshgen.grid_mode2b(v, *dims, 1)
+    want = np.ascontiguousarray(O.make_level_set3(v, t, o, dx, *dims, exact_band=1))
+    got = _lib.make_level_set3(v, t, o, dx, *dims, 1)
+    prof = _lib.last_profile()
+    assert prof["sparse_sweeps"] == (16 if mode == "sparse" else 8)
+    assert bits_equal(got, want), diff_report(got, want, dx)
+
+
 @pytest.mark.parametrize("nu,nv,dims", [(90, 31, (57, 33, 70)), (40, 21, (17, 40, 35)), (200, 61, (64, 48, 40))])
 def test_gpu_sweep_impls_agree_with_oracle(sweep_impl, nu, nv, dims):
     v, t = meshgen.bumpy_sphere(nu, nv)
